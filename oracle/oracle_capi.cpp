@@ -1,0 +1,421 @@
+// oracle/oracle_capi.cpp -- TEST INFRASTRUCTURE ONLY (see oracle_core.h).
+// Flat C entry points so pytest (ctypes) can drive the CPU restatement. Nodes
+// are addressed by their index in the pubkey array the caller passed in.
+#include "oracle_sim.h"
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+using namespace orc;
+
+namespace {
+Pubkey pk_at(const uint8_t* p, size_t i = 0) {
+  Pubkey k;
+  std::memcpy(k.b, p + 32 * i, 32);
+  return k;
+}
+std::vector<Pubkey> pk_vec(const uint8_t* p, size_t n) {
+  std::vector<Pubkey> v(n);
+  for (size_t i = 0; i < n; ++i) v[i] = pk_at(p, i);
+  return v;
+}
+size_t put_pks(const std::vector<Pubkey>& v, uint8_t* out, size_t cap) {
+  for (size_t i = 0; i < v.size() && i < cap; ++i) std::memcpy(out + 32 * i, v[i].b, 32);
+  return v.size();
+}
+thread_local std::string g_err;
+
+struct StatsHandle {
+  GossipStats st;
+  size_t origin_index = 0;
+  PkMap<size_t> index;  // for per-node outputs
+};
+
+size_t put_f(const std::vector<double>& v, double* out, size_t cap) {
+  for (size_t i = 0; i < v.size() && i < cap; ++i) out[i] = v[i];
+  return v.size();
+}
+size_t put_u(const std::vector<uint64_t>& v, uint64_t* out, size_t cap) {
+  for (size_t i = 0; i < v.size() && i < cap; ++i) out[i] = v[i];
+  return v.size();
+}
+std::vector<uint64_t> hist_kv(const Histogram& h) {
+  std::vector<uint64_t> v;
+  for (auto& kv : h.entries) { v.push_back(kv.first); v.push_back(kv.second); }
+  return v;
+}
+}  // namespace
+
+extern "C" {
+
+const char* or_last_error() { return g_err.c_str(); }
+
+// ------------------------------------------------------------- RNG ----
+void* or_chacha_new(const uint8_t* seed) { return new ChaCha20Rng(seed); }
+void* or_philox_stream_new(uint64_t seed, uint32_t purpose, uint32_t a, uint32_t b) {
+  return new PhiloxStream(seed, purpose, a, b);
+}
+void or_rng_free(void* r) { delete (Rng*)r; }
+uint64_t or_rng_next_u64(void* r) { return ((Rng*)r)->next_u64(); }
+uint64_t or_gen_range(void* r, uint64_t lo, uint64_t hi) { return sample_single_u64(lo, hi, *(Rng*)r); }
+double or_gen_f64(void* r) { return gen_f64(*(Rng*)r); }
+void or_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) { philox4x32_10(ctr, key, out); }
+int or_base58(const uint8_t* pk, char* out) {
+  std::string s = base58(pk_at(pk));
+  std::memcpy(out, s.c_str(), s.size() + 1);
+  return (int)s.size();
+}
+void or_pubkey_from_counter(uint64_t i, uint8_t* out) { std::memcpy(out, pubkey_from_counter(i).b, 32); }
+int or_stake_bucket(uint64_t stake, int has) { return get_stake_bucket(has ? &stake : nullptr); }
+
+void* or_stakes_new(const uint8_t* pks, const uint64_t* vals, size_t n) {
+  auto* s = new Stakes();
+  for (size_t i = 0; i < n; ++i) (*s)[pk_at(pks, i)] = vals[i];
+  return s;
+}
+void or_stakes_free(void* s) { delete (Stakes*)s; }
+
+// ------------------------------------------------ PushActiveSetEntry ----
+void* or_entry_new() { return new PushActiveSetEntry(); }
+void or_entry_free(void* e) { delete (PushActiveSetEntry*)e; }
+void or_entry_rotate(void* e, void* rng, size_t size, const uint8_t* nodes, const uint64_t* weights, size_t n) {
+  std::vector<uint64_t> w(weights, weights + n);
+  ((PushActiveSetEntry*)e)->rotate(*(Rng*)rng, size, pk_vec(nodes, n), w);
+}
+size_t or_entry_keys(void* e, uint8_t* out, size_t cap) { return put_pks(((PushActiveSetEntry*)e)->keys, out, cap); }
+size_t or_entry_get_nodes(void* e, const uint8_t* origin, int force, uint8_t* out, size_t cap) {
+  auto v = ((PushActiveSetEntry*)e)->get_nodes(pk_at(origin), [&](const Pubkey&) { return force != 0; });
+  return put_pks(v, out, cap);
+}
+void or_entry_prune(void* e, const uint8_t* node, const uint8_t* origin) {
+  ((PushActiveSetEntry*)e)->prune(pk_at(node), pk_at(origin));
+}
+int or_entry_filter_contains(void* e, const uint8_t* node, const uint8_t* key) {
+  auto* en = (PushActiveSetEntry*)e;
+  auto it = en->filters.find(pk_at(node));
+  if (it == en->filters.end()) return -1;
+  return it->second.count(pk_at(key)) ? 1 : 0;
+}
+
+// ------------------------------------------------------ PushActiveSet ----
+void* or_pas_new() { return new PushActiveSet(); }
+void or_pas_free(void* p) { delete (PushActiveSet*)p; }
+void or_pas_rotate(void* p, void* rng, size_t size, const uint8_t* nodes, size_t n, void* stakes) {
+  ((PushActiveSet*)p)->rotate([&](int) -> Rng& { return *(Rng*)rng; }, size, pk_vec(nodes, n), *(Stakes*)stakes);
+}
+size_t or_pas_get_nodes(void* p, const uint8_t* self, const uint8_t* origin, void* stakes, uint8_t* out, size_t cap) {
+  return put_pks(((PushActiveSet*)p)->get_nodes(pk_at(self), pk_at(origin), *(Stakes*)stakes), out, cap);
+}
+void or_pas_prune(void* p, const uint8_t* self, const uint8_t* node, const uint8_t* origins, size_t no, void* stakes) {
+  ((PushActiveSet*)p)->prune(pk_at(self), pk_at(node), pk_vec(origins, no), *(Stakes*)stakes);
+}
+size_t or_pas_entry_keys(void* p, int k, uint8_t* out, size_t cap) {
+  return put_pks(((PushActiveSet*)p)->e[k].keys, out, cap);
+}
+int or_pas_filter_contains(void* p, int k, const uint8_t* node, const uint8_t* key) {
+  return or_entry_filter_contains(&((PushActiveSet*)p)->e[k], node, key);
+}
+
+// ------------------------------------------------------ ReceivedCache ----
+void* or_rc_new() { return new ReceivedCache(); }
+void or_rc_free(void* r) { delete (ReceivedCache*)r; }
+void* or_rc_clone(void* r) { return new ReceivedCache(*(ReceivedCache*)r); }
+void or_rc_record(void* r, const uint8_t* origin, const uint8_t* node, size_t dups) {
+  ((ReceivedCache*)r)->record(pk_at(origin), pk_at(node), dups);
+}
+long or_rc_entry(void* r, const uint8_t* origin, uint64_t* upserts, uint8_t* nodes, uint64_t* scores, size_t cap) {
+  auto* rc = (ReceivedCache*)r;
+  auto it = rc->m.find(pk_at(origin));
+  if (it == rc->m.end()) return -1;
+  *upserts = it->second.num_upserts;
+  std::vector<std::pair<Pubkey, uint64_t>> v(it->second.nodes.begin(), it->second.nodes.end());
+  std::sort(v.begin(), v.end(), [](auto& a, auto& b) { return a.first < b.first; });
+  for (size_t i = 0; i < v.size() && i < cap; ++i) {
+    std::memcpy(nodes + 32 * i, v[i].first.b, 32);
+    scores[i] = v[i].second;
+  }
+  return (long)v.size();
+}
+size_t or_rc_prune(void* r, const uint8_t* self, const uint8_t* origin, double thr, size_t min_ingress, void* stakes,
+                   uint8_t* out, size_t cap) {
+  auto v = ((ReceivedCache*)r)->prune(pk_at(self), pk_at(origin), thr, min_ingress, *(Stakes*)stakes,
+                                      [](const Pubkey& k) { return (uint64_t)0 * k.b[0]; });
+  return put_pks(v, out, cap);
+}
+
+// ---------------------------------------------------------------- Sim ----
+void* or_sim_new(int mode, uint64_t seed, const uint8_t* pks, const uint64_t* stakes, size_t n, size_t fanout) {
+  return new Sim((Mode)mode, seed, pk_vec(pks, n), std::vector<uint64_t>(stakes, stakes + n), fanout);
+}
+void or_sim_free(void* s) { delete (Sim*)s; }
+void or_sim_init_compat(void* s, void* rng, size_t asz) { ((Sim*)s)->init_compat(*(Rng*)rng, asz); }
+void or_sim_init_philox(void* s, size_t asz) { ((Sim*)s)->init_philox(asz); }
+void or_sim_run_gossip(void* sp, size_t origin) {
+  Sim* s = (Sim*)sp;
+  auto nm = s->node_map();
+  s->cluster.run_gossip(s->nodes[origin].pk, s->stakes, nm);
+}
+void or_sim_consume(void* sp, size_t origin) {
+  Sim* s = (Sim*)sp;
+  s->cluster.consume_messages(s->nodes[origin].pk, s->nodes,
+                              [&](const Pubkey& k) -> const std::string& { return s->b58.at(k); });
+}
+void or_sim_send_prunes(void* sp, size_t origin, double thr, size_t min_ingress) {
+  Sim* s = (Sim*)sp;
+  s->cluster.send_prunes(s->nodes[origin].pk, s->nodes, thr, min_ingress, s->stakes,
+                         [&](const Pubkey& k) { return s->rank.at(k); });
+}
+void or_sim_prune_connections(void* sp) {
+  Sim* s = (Sim*)sp;
+  auto nm = s->node_map();
+  s->cluster.prune_connections(nm, s->stakes);
+}
+void or_sim_chance_to_rotate(void* s, size_t asz, double p, uint32_t round, void* compat_rng) {
+  ((Sim*)s)->chance_to_rotate(asz, p, round, (Rng*)compat_rng);
+}
+long or_sim_fail_nodes(void* s, double f) {
+  try { return (long)((Sim*)s)->fail_nodes(f); } catch (std::exception& e) { g_err = e.what(); return -1; }
+}
+size_t or_sim_find_nth_largest(void* sp, size_t n) {
+  Sim* s = (Sim*)sp;
+  const Node* nd = s->find_nth_largest(n);
+  return nd ? s->index.at(nd->pk) : (size_t)-1;
+}
+size_t or_sim_rank(void* sp, size_t idx) { Sim* s = (Sim*)sp; return s->rank.at(s->nodes[idx].pk); }
+size_t or_sim_visited_len(void* s) { return ((Sim*)s)->cluster.visited.size(); }
+void or_sim_distances(void* sp, uint64_t* out) {
+  Sim* s = (Sim*)sp;
+  for (size_t i = 0; i < s->nodes.size(); ++i) {
+    auto it = s->cluster.distances.find(s->nodes[i].pk);
+    out[i] = it == s->cluster.distances.end() ? UINT64_MAX : it->second;
+  }
+}
+long or_sim_orders(void* sp, size_t dest, uint32_t* src, uint64_t* hops, size_t cap) {
+  Sim* s = (Sim*)sp;
+  auto it = s->cluster.orders.find(s->nodes[dest].pk);
+  if (it == s->cluster.orders.end()) return -1;
+  std::vector<std::pair<uint64_t, uint64_t>> v;  // (hop, rank) -- the consume order
+  for (auto& kv : it->second) v.push_back({kv.second, s->rank.at(kv.first)});
+  std::sort(v.begin(), v.end());
+  for (size_t i = 0; i < v.size() && i < cap; ++i) {
+    src[i] = (uint32_t)s->index.at(s->by_rank[v[i].second]);
+    hops[i] = v[i].first;
+  }
+  return (long)v.size();
+}
+static long set_out(Sim* s, const PkMap<PkSet>& m, size_t key, uint32_t* out, size_t cap) {
+  auto it = m.find(s->nodes[key].pk);
+  if (it == m.end()) return -1;
+  std::vector<uint32_t> v;
+  for (auto& p : it->second) v.push_back((uint32_t)s->index.at(p));
+  std::sort(v.begin(), v.end());
+  for (size_t i = 0; i < v.size() && i < cap; ++i) out[i] = v[i];
+  return (long)v.size();
+}
+long or_sim_pushes(void* s, size_t src, uint32_t* out, size_t cap) {
+  return set_out((Sim*)s, ((Sim*)s)->cluster.pushes, src, out, cap);
+}
+long or_sim_mst(void* s, size_t src, uint32_t* out, size_t cap) {
+  return set_out((Sim*)s, ((Sim*)s)->cluster.mst, src, out, cap);
+}
+size_t or_sim_prunes_len(void* s) { return ((Sim*)s)->cluster.prunes.size(); }
+size_t or_sim_prunes(void* sp, uint32_t* pruner, uint32_t* prunee, size_t cap) {
+  Sim* s = (Sim*)sp;
+  std::vector<std::pair<uint32_t, uint32_t>> v;
+  for (auto& kv : s->cluster.prunes)
+    for (auto& pe : kv.second) v.push_back({(uint32_t)s->index.at(kv.first), (uint32_t)s->index.at(pe.first)});
+  std::sort(v.begin(), v.end());
+  for (size_t i = 0; i < v.size() && i < cap; ++i) { pruner[i] = v[i].first; prunee[i] = v[i].second; }
+  return v.size();
+}
+void or_sim_counters(void* sp, uint64_t* egress, uint64_t* ingress, uint64_t* prune_sent) {
+  Sim* s = (Sim*)sp;
+  auto fill = [&](const PkMap<uint64_t>& m, uint64_t* out) {
+    for (size_t i = 0; i < s->nodes.size(); ++i) {
+      auto it = m.find(s->nodes[i].pk);
+      out[i] = it == m.end() ? UINT64_MAX : it->second;
+    }
+  };
+  fill(s->cluster.egress_message_count, egress);
+  fill(s->cluster.ingress_message_count, ingress);
+  fill(s->cluster.prune_messages_sent, prune_sent);
+}
+int or_sim_rmr(void* s, double* r, uint64_t* m, uint64_t* n) {
+  return ((Sim*)s)->cluster.relative_message_redundancy(r, m, n) ? 0 : -1;
+}
+uint64_t or_sim_rmr_m(void* s) { return ((Sim*)s)->cluster.rmr_m; }
+uint64_t or_sim_rmr_n(void* s) { return ((Sim*)s)->cluster.rmr_n; }
+double or_sim_coverage(void* sp, size_t* left_out) {
+  Sim* s = (Sim*)sp;
+  auto c = s->cluster.coverage(s->stakes);
+  *left_out = c.second;
+  return c.first;
+}
+size_t or_sim_stranded(void* sp, uint32_t* out, size_t cap) {
+  Sim* s = (Sim*)sp;
+  std::vector<uint32_t> v;
+  for (auto& p : s->cluster.stranded_nodes()) v.push_back((uint32_t)s->index.at(p));
+  std::sort(v.begin(), v.end());
+  for (size_t i = 0; i < v.size() && i < cap; ++i) out[i] = v[i];
+  return v.size();
+}
+long or_sim_entry(void* sp, size_t node, int k, uint32_t* peers, size_t cap) {
+  Sim* s = (Sim*)sp;
+  auto& keys = s->nodes[node].active_set.e[k].keys;
+  for (size_t i = 0; i < keys.size() && i < cap; ++i) peers[i] = (uint32_t)s->index.at(keys[i]);
+  return (long)keys.size();
+}
+// 1 if `origin` is in the filter of `peer` inside entry k of `node` (prune state).
+int or_sim_entry_pruned(void* sp, size_t node, int k, size_t peer, size_t origin) {
+  Sim* s = (Sim*)sp;
+  auto& f = s->nodes[node].active_set.e[k].filters;
+  auto it = f.find(s->nodes[peer].pk);
+  if (it == f.end()) return -1;
+  return it->second.count(s->nodes[origin].pk) ? 1 : 0;
+}
+long or_sim_cache(void* sp, size_t node, size_t origin, uint64_t* upserts, uint32_t* keys, uint64_t* scores,
+                  size_t cap) {
+  Sim* s = (Sim*)sp;
+  auto& rc = s->nodes[node].received_cache;
+  auto it = rc.m.find(s->nodes[origin].pk);
+  if (it == rc.m.end()) return -1;
+  *upserts = it->second.num_upserts;
+  std::vector<std::pair<uint32_t, uint64_t>> v;
+  for (auto& kv : it->second.nodes) v.push_back({(uint32_t)s->index.at(kv.first), kv.second});
+  std::sort(v.begin(), v.end());
+  for (size_t i = 0; i < v.size() && i < cap; ++i) { keys[i] = v[i].first; scores[i] = v[i].second; }
+  return (long)v.size();
+}
+void or_sim_failed(void* sp, uint8_t* out) {
+  Sim* s = (Sim*)sp;
+  for (size_t i = 0; i < s->nodes.size(); ++i) out[i] = s->nodes[i].failed;
+}
+size_t or_sim_total_prunes(void* s) { return ((Sim*)s)->cluster.total_prunes; }
+
+// --------------------------------------------------------------- stats ----
+void* or_stats_new() { return new StatsHandle(); }
+void or_stats_free(void* h) { delete (StatsHandle*)h; }
+void or_stats_insert_hops(void* h, const uint64_t* d, size_t n) {
+  PkMap<uint64_t> m;
+  for (size_t i = 0; i < n; ++i) m[pubkey_from_counter(i + 1)] = d[i];
+  ((StatsHandle*)h)->st.insert_hops_stat(m);
+}
+void or_stats_insert_coverage(void* h, double v) { ((StatsHandle*)h)->st.coverage.collection.push_back(v); }
+void or_stats_insert_rmr(void* h, double v) { ((StatsHandle*)h)->st.rmr.collection.push_back(v); }
+void or_stats_insert_stranded(void* h, const uint8_t* pks, size_t n, void* stakes) {
+  ((StatsHandle*)h)->st.stranded.insert_nodes(pk_vec(pks, n), *(Stakes*)stakes);
+}
+void or_stats_branching(void* h, const uint64_t* set_sizes, size_t n_srcs) {
+  PkMap<PkSet> pushes;
+  for (size_t i = 0; i < n_srcs; ++i) {
+    PkSet s;
+    for (uint64_t j = 0; j < set_sizes[i]; ++j) s.insert(pubkey_from_counter(j + 1));
+    pushes[pubkey_from_counter(1000000 + i)] = s;
+  }
+  ((StatsHandle*)h)->st.calculate_branching(pushes);
+}
+void or_stats_calculate(void* h) { ((StatsHandle*)h)->st.run_all_calculations(); }
+
+void* or_run_simulation(const uint8_t* pks, const uint64_t* stakes, size_t n, size_t fanout, size_t asz,
+                        size_t iterations, size_t origin_rank, double p, double thr, size_t min_ingress,
+                        uint64_t nb_stranded, uint64_t nb_message, uint64_t nb_hops, double fraction_to_fail,
+                        size_t when_to_fail, int test_type, size_t warm_up, uint64_t seed) {
+  SimConfig c;
+  c.push_fanout = fanout; c.active_set_size = asz; c.iterations = iterations; c.origin_rank = origin_rank;
+  c.rotation_probability = p; c.prune_stake_threshold = thr; c.min_ingress_nodes = min_ingress;
+  c.num_buckets_stranded = nb_stranded; c.num_buckets_message = nb_message; c.num_buckets_hops = nb_hops;
+  c.fraction_to_fail = fraction_to_fail; c.when_to_fail = when_to_fail; c.test_type = test_type;
+  c.warm_up_rounds = warm_up; c.seed = seed;
+  auto* h = new StatsHandle();
+  auto v = pk_vec(pks, n);
+  for (size_t i = 0; i < n; ++i) h->index[v[i]] = i;
+  try {
+    Pubkey origin;
+    run_simulation(c, v, std::vector<uint64_t>(stakes, stakes + n), h->st, &origin);
+    h->origin_index = h->index.at(origin);
+  } catch (std::exception& e) {
+    g_err = e.what();
+    delete h;
+    return nullptr;
+  }
+  return h;
+}
+
+size_t or_res_f64(void* hp, const char* name, double* out, size_t cap) {
+  auto* h = (StatsHandle*)hp;
+  auto& st = h->st;
+  std::string n(name);
+  auto s4 = [](const StatCollection& c) { return std::vector<double>{c.mean, c.median, c.max, c.min}; };
+  if (n == "coverage") return put_f(st.coverage.collection, out, cap);
+  if (n == "rmr") return put_f(st.rmr.collection, out, cap);
+  if (n == "branching") return put_f(st.branching.collection, out, cap);
+  if (n == "coverage_stats") return put_f(s4(st.coverage), out, cap);
+  if (n == "rmr_stats") return put_f(s4(st.rmr), out, cap);
+  if (n == "branching_stats") return put_f(s4(st.branching), out, cap);
+  if (n == "hop_mean" || n == "hop_median") {
+    std::vector<double> v;
+    for (auto& x : st.per_round_hops) v.push_back(n == "hop_mean" ? x.mean : x.median);
+    return put_f(v, out, cap);
+  }
+  if (n == "aggregate_hops") return put_f({st.aggregate_hops.mean, st.aggregate_hops.median}, out, cap);
+  if (n == "ldh") return put_f({st.ldh.mean, st.ldh.median}, out, cap);
+  if (n == "stranded_round_mean" || n == "stranded_round_median") {
+    std::vector<double> v;
+    for (auto& x : st.stranded.per_iter) v.push_back(n == "stranded_round_mean" ? x.mean : x.median);
+    return put_f(v, out, cap);
+  }
+  if (n == "stranded") {
+    auto& s = st.stranded;
+    // get_stranded_stats order (gossip_stats.rs:1572-1602), f64 members only
+    return put_f({s.stranded_iterations_per_node, s.mean_stranded_per_iteration, s.mean_iters_per_stranded_node,
+                  s.median_iters_per_stranded_node, s.mean_stake, s.median_stake, s.weighted_mean_stake,
+                  s.weighted_median_stake},
+                 out, cap);
+  }
+  return (size_t)-1;
+}
+
+size_t or_res_u64(void* hp, const char* name, uint64_t* out, size_t cap) {
+  auto* h = (StatsHandle*)hp;
+  auto& st = h->st;
+  std::string n(name);
+  if (n == "origin") return put_u({h->origin_index}, out, cap);
+  if (n == "hop_max" || n == "hop_min") {
+    std::vector<uint64_t> v;
+    for (auto& x : st.per_round_hops) v.push_back(n == "hop_max" ? x.max : x.min);
+    return put_u(v, out, cap);
+  }
+  if (n == "aggregate_hops") return put_u({st.aggregate_hops.max, st.aggregate_hops.min}, out, cap);
+  if (n == "ldh") return put_u({st.ldh.max, st.ldh.min}, out, cap);
+  if (n == "stranded_round_count" || n == "stranded_round_max" || n == "stranded_round_min") {
+    std::vector<uint64_t> v;
+    for (auto& x : st.stranded.per_iter)
+      v.push_back(n == "stranded_round_count" ? x.count : n == "stranded_round_max" ? x.max : x.min);
+    return put_u(v, out, cap);
+  }
+  if (n == "stranded") {
+    auto& s = st.stranded;
+    return put_u({s.total_stranded_iterations, (uint64_t)s.stranded_nodes.size(), s.max_stake, s.min_stake}, out, cap);
+  }
+  if (n == "stranded_times") {  // (node index, times) sorted by index
+    std::vector<std::pair<uint64_t, uint64_t>> v;
+    for (auto& kv : st.stranded.stranded_nodes) v.push_back({h->index.at(kv.first), kv.second.second});
+    std::sort(v.begin(), v.end());
+    std::vector<uint64_t> f;
+    for (auto& p : v) { f.push_back(p.first); f.push_back(p.second); }
+    return put_u(f, out, cap);
+  }
+  if (n == "hops_hist") return put_u(hist_kv(st.hops_histogram), out, cap);
+  if (n == "stranded_hist") return put_u(hist_kv(st.stranded.histogram), out, cap);
+  if (n == "validator_hist") return put_u(hist_kv(st.validator_stake_distribution), out, cap);
+  if (n == "egress_hist") return put_u(hist_kv(st.egress.histogram), out, cap);
+  if (n == "ingress_hist") return put_u(hist_kv(st.ingress.histogram), out, cap);
+  if (n == "prune_hist") return put_u(hist_kv(st.prune.histogram), out, cap);
+  if (n == "egress_cpb") return put_u(st.egress.count_per_bucket, out, cap);
+  if (n == "hist_errors")
+    return put_u({(uint64_t)st.hops_histogram.errors, (uint64_t)st.stranded.histogram.errors}, out, cap);
+  if (n == "failed_count") return put_u({(uint64_t)st.failed_count}, out, cap);
+  return (size_t)-1;
+}
+
+}  // extern "C"
