@@ -1,0 +1,742 @@
+// gs_engine.hip -- engine lifetime, the C ABI of include/gossip_hip.h and readbacks.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "gs_device.h"
+#include "gs_internal.h"
+
+using namespace gs;
+
+namespace gs {
+size_t bfs_wg_lds_bytes(uint32_t N);
+}
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPC(expr)                                                                              \
+  do {                                                                                          \
+    hipError_t _r = (expr);                                                                     \
+    if (_r != hipSuccess)                                                                       \
+      return fail(GS_EHIP, std::string(#expr) + ": " + hipGetErrorString(_r));                  \
+  } while (0)
+
+void Engine::tbegin(const char* fam, hipEvent_t* a) {
+  *a = nullptr;
+  if (!(prm.flags & GS_FLAG_PROFILE)) return;
+  hipEventCreate(a);
+  hipEventRecord(*a, st);
+  (void)fam;
+}
+void Engine::tend(const char* fam, hipEvent_t a) {
+  if (!a) return;
+  hipEvent_t b;
+  hipEventCreate(&b);
+  hipEventRecord(b, st);
+  timers[fam].ev.push_back({a, b});
+}
+
+template <class T>
+static int dalloc(Engine& e, T** p, size_t count, int fill = 0) {
+  size_t bytes = count * sizeof(T);
+  if (bytes == 0) bytes = 16;
+  void* ptr = nullptr;
+  hipError_t r = hipMalloc(&ptr, bytes);
+  if (r != hipSuccess) return fail(GS_ENOMEM, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(r));
+  e.allocs.push_back(ptr);
+  e.dev_bytes += bytes;
+  r = hipMemsetAsync(ptr, fill, bytes, e.st);
+  if (r != hipSuccess) return fail(GS_EHIP, std::string("hipMemsetAsync: ") + hipGetErrorString(r));
+  *p = (T*)ptr;
+  return GS_OK;
+}
+#define ALLOC(ptr, count, fill)                   \
+  do {                                            \
+    int _s = dalloc(*e, &(ptr), (count), (fill)); \
+    if (_s) { destroy_engine(e); return _s; }     \
+  } while (0)
+
+static void destroy_engine(Engine* e) {
+  if (!e) return;
+  if (e->st) hipStreamSynchronize(e->st);
+  for (void* p : e->allocs) hipFree(p);
+  if (e->h_err) hipHostFree(e->h_err);
+  for (auto& kv : e->timers)
+    for (auto& pr : kv.second.ev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+  if (e->st) hipStreamDestroy(e->st);
+  delete e;
+}
+
+// Sorts (key, id) pairs on the device (stable, so ties stay in id order) and
+// returns the sorted ids in out_ids.
+static int sort_ids_by_key(Engine& e, const uint64_t* keys_in, uint32_t* out_ids) {
+  uint64_t *kin = nullptr, *kout = nullptr;
+  uint32_t *vin = nullptr;
+  hipError_t r;
+  if ((r = hipMalloc(&kin, e.N * 8ull)) != hipSuccess) return fail(GS_ENOMEM, "sort alloc");
+  hipMalloc(&kout, e.N * 8ull);
+  hipMalloc(&vin, e.N * 4ull);
+  if (!kout || !vin) return fail(GS_ENOMEM, "sort alloc");
+  hipMemcpyAsync(kin, keys_in, e.N * 8ull, hipMemcpyDeviceToDevice, e.st);
+  std::vector<uint32_t> ids(e.N);
+  for (uint32_t i = 0; i < e.N; ++i) ids[i] = i;
+  hipMemcpyAsync(vin, ids.data(), e.N * 4ull, hipMemcpyHostToDevice, e.st);
+  size_t tmp_bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, out_ids, (int)e.N, 0, 64, e.st);
+  void* tmp = nullptr;
+  hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16);
+  r = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, out_ids, (int)e.N, 0, 64, e.st);
+  hipStreamSynchronize(e.st);
+  hipFree(tmp); hipFree(kin); hipFree(kout); hipFree(vin);
+  if (r != hipSuccess) return fail(GS_EHIP, std::string("radix sort: ") + hipGetErrorString(r));
+  return GS_OK;
+}
+
+static int check_err(Engine* e) {
+  HIPC(hipMemcpyAsync(e->h_err, e->err, 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  const uint32_t f = e->h_err[0];
+  if (f & ERR_INBOUND)
+    return fail(GS_ERANGE, "inbound capacity exceeded: a node received more than " + std::to_string(e->capin) +
+                               " pushes in one round; recreate the engine with a larger inbound_capacity");
+  if (f & ERR_CACHE) return fail(GS_ERANGE, "received-cache capacity (96 keys) exceeded");
+  if (f & ERR_DEPTH) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
+  return GS_OK;
+}
+
+extern "C" {
+
+const char* gs_last_error(void) { return g_err.c_str(); }
+
+int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t n_slots, gs_engine** out) {
+  if (!prm || !stakes || !out) return fail(GS_EINVAL, "null argument");
+  *out = nullptr;
+  if (n < 2 || n > GS_MAX_NODES) return fail(GS_EINVAL, "n_nodes must be in [2, 2^24-1]");
+  if (n_slots < 1) return fail(GS_EINVAL, "n_slots must be >= 1");
+  if (prm->active_set_size < 1 || prm->active_set_size > GS_MAX_ACTIVE_SET_SIZE)
+    return fail(GS_EINVAL, "active_set_size must be in [1, 32]");
+  if (prm->push_fanout < 1) return fail(GS_EINVAL, "push_fanout must be >= 1");
+  if (!(prm->rotation_probability >= 0.0 && prm->rotation_probability <= 1.0))
+    return fail(GS_EINVAL, "rotation_probability must be in [0, 1]");
+  if ((uint64_t)n * n_slots >= (1ull << 32)) return fail(GS_EINVAL, "n_nodes * n_slots must be < 2^32");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(GS_EHIP, "no HIP device visible (the engine has no CPU fallback)");
+  if (prm->device < 0 || prm->device >= ndev) return fail(GS_EINVAL, "device ordinal out of range");
+  HIPC(hipSetDevice(prm->device));
+
+  Engine* e = new (std::nothrow) Engine();
+  if (!e) return fail(GS_ENOMEM, "host allocation");
+  e->prm = *prm;
+  e->N = n;
+  e->S = n_slots;
+  e->PAIRS = (size_t)n * n_slots;
+  e->ASZ = prm->active_set_size;
+  e->ASZP = (e->ASZ + 3) & ~3u;
+  e->fanout = prm->push_fanout;
+  e->capin = prm->inbound_capacity ? prm->inbound_capacity : 64;
+  if (hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) {
+    destroy_engine(e);
+    return fail(GS_EHIP, "hipStreamCreate");
+  }
+  if (hipHostMalloc(&e->h_err, 64) != hipSuccess) { destroy_engine(e); return fail(GS_ENOMEM, "pinned alloc"); }
+  std::memset(e->h_err, 0, 64);
+
+  uint32_t mode = prm->bfs_mode;
+  const size_t lds = bfs_wg_lds_bytes(n);
+  if (mode == GS_BFS_AUTO) mode = (n <= 8192 && n_slots >= 64) ? GS_BFS_WORKGROUP : GS_BFS_LEVEL;
+  if (mode == GS_BFS_WORKGROUP && (n > 65535 || lds > 160 * 1024)) {
+    destroy_engine(e);
+    return fail(GS_EINVAL, "workgroup BFS needs the per-slot state (9 B/node) to fit in 160 KiB of LDS");
+  }
+  if (mode != GS_BFS_WORKGROUP && mode != GS_BFS_LEVEL) { destroy_engine(e); return fail(GS_EINVAL, "bfs_mode"); }
+  e->bfs_mode = mode;
+
+  const size_t N = n, S = n_slots, PAIRS = e->PAIRS;
+  ALLOC(e->stake, N, 0);
+  ALLOC(e->bucket, N, 0);
+  ALLOC(e->P, (size_t)NB * (N + 1), 0);
+  ALLOC(e->peers, N * NB * e->ASZP, 0);
+  ALLOC(e->hl, N * NB, 0);
+  ALLOC(e->frank, N, 0);
+  ALLOC(e->srank, N, 0);
+  ALLOC(e->by_srank, N, 0);
+  ALLOC(e->origin, S, 0);
+  ALLOC(e->obkt, S, 0);
+  ALLOC(e->min_ingress, S, 0);
+  ALLOC(e->thr, S, 0);
+  ALLOC(e->nfail, S, 0);
+  ALLOC(e->slot_prunes, S, 0);
+  ALLOC(e->hops, PAIRS, 0xFF);
+  ALLOC(e->cnt, PAIRS, 0);
+  ALLOC(e->mask, PAIRS, 0);
+  ALLOC(e->inb, (size_t)e->capin * PAIRS, 0);
+  ALLOC(e->cmeta, PAIRS, 0);
+  ALLOC(e->ckey, (size_t)CACHE_CAP * PAIRS, 0);
+  ALLOC(e->cscore, (size_t)CACHE_CAP * PAIRS, 0);
+  ALLOC(e->egress, PAIRS, 0);
+  ALLOC(e->prune_round, PAIRS, 0);
+  ALLOC(e->egress_acc, PAIRS, 0);
+  ALLOC(e->ingress_acc, PAIRS, 0);
+  ALLOC(e->prune_acc, PAIRS, 0);
+  ALLOC(e->strand, PAIRS, 0);
+  if (mode == GS_BFS_LEVEL) {
+    ALLOC(e->q[0], PAIRS, 0);
+    ALLOC(e->q[1], PAIRS, 0);
+  }
+  ALLOC(e->lvl, 256, 0);
+  ALLOC(e->rot_list, N, 0);
+  ALLOC(e->rot_count, 1, 0);
+  ALLOC(e->rot_changed, N * NB, 0);
+  ALLOC(e->rs_u32, S * 4, 0);
+  ALLOC(e->rs_ssum, S, 0);
+  ALLOC(e->rs_hist, S * 256, 0);
+  ALLOC(e->hist_acc, S * 256, 0);
+  e->bm_words = (n + 31) / 32;
+  ALLOC(e->bm, S * e->bm_words, 0);
+  e->sum_cap = 64;
+  ALLOC(e->sum, (size_t)e->sum_cap * S, 0);
+  ALLOC(e->err, 4, 0);
+
+  // stakes, buckets and the static rotation prefix sums
+  std::vector<uint8_t> b(N);
+  for (size_t i = 0; i < N; ++i) b[i] = (uint8_t)stake_bucket(stakes[i]);
+  if (hipMemcpyAsync(e->stake, stakes, N * 8, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      hipMemcpyAsync(e->bucket, b.data(), N, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      launch_prefix_weights(*e) != hipSuccess) {
+    destroy_engine(e);
+    return fail(GS_EHIP, "upload / prefix-weights launch failed");
+  }
+  // stake rank (ascending stake, ties by id) for the stranded-stake order statistics
+  int s = sort_ids_by_key(*e, e->stake, e->by_srank);
+  if (s) { destroy_engine(e); return s; }
+  if (launch_scatter_rank(*e, e->by_srank, e->srank) != hipSuccess) {
+    destroy_engine(e);
+    return fail(GS_EHIP, "stake-rank scatter");
+  }
+  if (hipStreamSynchronize(e->st) != hipSuccess) { destroy_engine(e); return fail(GS_EHIP, "create sync"); }
+  *out = reinterpret_cast<gs_engine*>(e);
+  return GS_OK;
+}
+
+void gs_destroy(gs_engine* eh) { destroy_engine(reinterpret_cast<Engine*>(eh)); }
+
+#define ENGINE(eh)                                              \
+  Engine* e = reinterpret_cast<Engine*>(eh);                    \
+  if (!e) return fail(GS_EINVAL, "null engine");                \
+  HIPC(hipSetDevice(e->prm.device));
+
+static int reset_pair_state(Engine* e) {
+  HIPC(hipMemsetAsync(e->mask, 0, e->PAIRS * 4, e->st));
+  HIPC(hipMemsetAsync(e->cmeta, 0, e->PAIRS * 4, e->st));
+  HIPC(hipMemsetAsync(e->egress_acc, 0, e->PAIRS * 4, e->st));
+  HIPC(hipMemsetAsync(e->ingress_acc, 0, e->PAIRS * 4, e->st));
+  HIPC(hipMemsetAsync(e->prune_acc, 0, e->PAIRS * 4, e->st));
+  HIPC(hipMemsetAsync(e->strand, 0, e->PAIRS * 4, e->st));
+  HIPC(hipMemsetAsync(e->hist_acc, 0, (size_t)e->S * 256 * 8, e->st));
+  HIPC(hipMemsetAsync(e->hops, 0xFF, e->PAIRS, e->st));
+  HIPC(hipMemsetAsync(e->cnt, 0, e->PAIRS * 4, e->st));
+  HIPC(hipMemsetAsync(e->prune_round, 0, e->PAIRS, e->st));
+  e->sum_used = 0;
+  e->h_sum.clear();
+  return GS_OK;
+}
+
+int gs_set_slots(gs_engine* eh, const gs_slot* slots, uint32_t n_slots) {
+  ENGINE(eh);
+  if (!slots || n_slots != e->S) return fail(GS_EINVAL, "gs_set_slots: need exactly n_slots entries");
+  std::vector<uint32_t> org(e->S), mi(e->S);
+  std::vector<uint8_t> ob(e->S);
+  std::vector<double> thr(e->S);
+  std::vector<uint8_t> bh(e->N);
+  HIPC(hipMemcpyAsync(bh.data(), e->bucket, e->N, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  for (uint32_t o = 0; o < e->S; ++o) {
+    if (slots[o].origin >= e->N) return fail(GS_EINVAL, "slot origin out of range");
+    if (!(slots[o].prune_stake_threshold >= 0.0) || std::isinf(slots[o].prune_stake_threshold))
+      return fail(GS_EINVAL, "prune_stake_threshold must be finite and >= 0");
+    org[o] = slots[o].origin;
+    ob[o] = bh[slots[o].origin];
+    mi[o] = slots[o].min_ingress_nodes;
+    thr[o] = slots[o].prune_stake_threshold;
+  }
+  HIPC(hipMemcpyAsync(e->origin, org.data(), e->S * 4, hipMemcpyHostToDevice, e->st));
+  HIPC(hipMemcpyAsync(e->obkt, ob.data(), e->S, hipMemcpyHostToDevice, e->st));
+  HIPC(hipMemcpyAsync(e->min_ingress, mi.data(), e->S * 4, hipMemcpyHostToDevice, e->st));
+  HIPC(hipMemcpyAsync(e->thr, thr.data(), e->S * 8, hipMemcpyHostToDevice, e->st));
+  e->slots.assign(slots, slots + n_slots);
+  e->slots_set = true;
+  int r = reset_pair_state(e);
+  if (r) return r;
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_sync(gs_engine* eh) {
+  ENGINE(eh);
+  return check_err(e);
+}
+
+int gs_init_active_sets(gs_engine* eh) {
+  ENGINE(eh);
+  HIPC(launch_init_entries(*e));
+  HIPC(hipMemsetAsync(e->mask, 0, e->PAIRS * 4, e->st));
+  return GS_OK;
+}
+
+int gs_set_active_set_entry(gs_engine* eh, uint32_t node, uint32_t bucket, const uint32_t* peers, uint32_t len) {
+  ENGINE(eh);
+  if (node >= e->N || bucket >= (uint32_t)NB) return fail(GS_EINVAL, "node/bucket out of range");
+  if (len > e->ASZ) return fail(GS_ERANGE, "entry longer than active_set_size");
+  std::vector<uint32_t> row(e->ASZP, 0);
+  for (uint32_t i = 0; i < len; ++i) {
+    if (peers[i] >= e->N || peers[i] == node) return fail(GS_EINVAL, "bad peer id");
+    for (uint32_t j = 0; j < i; ++j)
+      if (peers[j] == peers[i]) return fail(GS_EINVAL, "duplicate peer in entry");
+    row[i] = peers[i];
+  }
+  const size_t ent = (size_t)node * NB + bucket;
+  uint16_t hv = (uint16_t)(len << 8);
+  HIPC(hipMemcpyAsync(e->peers + ent * e->ASZP, row.data(), e->ASZP * 4, hipMemcpyHostToDevice, e->st));
+  HIPC(hipMemcpyAsync(e->hl + ent, &hv, 2, hipMemcpyHostToDevice, e->st));
+  HIPC(launch_clear_slot_masks(*e, node, bucket, 0xFFFFFFFFu));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_get_active_set_entry(gs_engine* eh, uint32_t node, uint32_t bucket, uint32_t* peers, uint32_t cap,
+                            uint32_t* len) {
+  ENGINE(eh);
+  if (node >= e->N || bucket >= (uint32_t)NB) return fail(GS_EINVAL, "node/bucket out of range");
+  const size_t ent = (size_t)node * NB + bucket;
+  std::vector<uint32_t> row(e->ASZP);
+  uint16_t hv = 0;
+  HIPC(hipMemcpyAsync(row.data(), e->peers + ent * e->ASZP, e->ASZP * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(&hv, e->hl + ent, 2, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  const uint32_t head = hv & 0xFF, L = hv >> 8;
+  *len = L;
+  if (L > cap) return fail(GS_ERANGE, "peers buffer too small");
+  for (uint32_t j = 0; j < L; ++j) peers[j] = row[(head + j) % e->ASZ];
+  return GS_OK;
+}
+
+int gs_fail_nodes(gs_engine* eh, const double* fraction) {
+  ENGINE(eh);
+  if (!fraction) return fail(GS_EINVAL, "null fractions");
+  if (!e->failed_ranked) {
+    uint64_t* keys = nullptr;
+    uint32_t *ids = nullptr, *sorted = nullptr;
+    HIPC(hipMalloc(&keys, e->N * 8ull));
+    HIPC(hipMalloc(&ids, e->N * 4ull));
+    HIPC(hipMalloc(&sorted, e->N * 4ull));
+    HIPC(launch_fail_keys(*e, keys, ids));
+    int s = sort_ids_by_key(*e, keys, sorted);
+    if (s) return s;
+    HIPC(launch_scatter_rank(*e, sorted, e->frank));
+    HIPC(hipStreamSynchronize(e->st));
+    hipFree(keys); hipFree(ids); hipFree(sorted);
+    e->failed_ranked = true;
+  }
+  std::vector<uint32_t> nf(e->S);
+  HIPC(hipMemcpyAsync(nf.data(), e->nfail, e->S * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  for (uint32_t o = 0; o < e->S; ++o) {
+    const double f = fraction[o] * (double)e->N;  // (fraction * nodes.len() as f64) as usize
+    uint64_t k = (f > 0.0) ? (uint64_t)f : 0;     // saturating cast, NaN -> 0
+    if (f >= 1.8446744073709552e19) k = ~0ull;
+    if (k > e->N) return fail(GS_ERANGE, "fail_nodes: fraction * n exceeds the cluster (reference panics)");
+    nf[o] = std::max(nf[o], (uint32_t)k);
+  }
+  HIPC(hipMemcpyAsync(e->nfail, nf.data(), e->S * 4, hipMemcpyHostToDevice, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+static int need_slots(Engine* e) {
+  if (!e->slots_set) return fail(GS_ESTATE, "gs_set_slots has not been called");
+  return GS_OK;
+}
+
+static int do_bfs(Engine* e) {
+  hipEvent_t t0;
+  e->tbegin("bfs", &t0);
+  hipError_t r = launch_bfs(*e);
+  e->tend("bfs", t0);
+  if (r == hipErrorNotSupported) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
+  HIPC(r);
+  return GS_OK;
+}
+
+int gs_run_gossip(gs_engine* eh) {
+  ENGINE(eh);
+  if (int s = need_slots(e)) return s;
+  return do_bfs(e);
+}
+
+static int do_cp(Engine* e, bool c, bool p, bool a) {
+  hipEvent_t t0;
+  e->tbegin("consume", &t0);
+  hipError_t r = launch_consume_prune(*e, c, p, a);
+  e->tend("consume", t0);
+  HIPC(r);
+  return GS_OK;
+}
+int gs_consume_messages(gs_engine* eh) { ENGINE(eh); if (int s = need_slots(e)) return s; return do_cp(e, true, false, false); }
+int gs_send_prunes(gs_engine* eh) { ENGINE(eh); if (int s = need_slots(e)) return s; return do_cp(e, false, true, false); }
+int gs_prune_connections(gs_engine* eh) { ENGINE(eh); if (int s = need_slots(e)) return s; return do_cp(e, false, false, true); }
+
+int gs_chance_to_rotate(gs_engine* eh, uint32_t round) {
+  ENGINE(eh);
+  if (int s = need_slots(e)) return s;
+  if (round >= (1u << 27)) return fail(GS_ERANGE, "round index must be < 2^27");
+  hipEvent_t t0;
+  e->tbegin("rotate", &t0);
+  hipError_t r = launch_rotate(*e, round);
+  e->tend("rotate", t0);
+  HIPC(r);
+  return GS_OK;
+}
+
+static int drain_summaries(Engine* e) {
+  if (!e->sum_used) return GS_OK;
+  size_t n = (size_t)e->sum_used * e->S;
+  size_t old = e->h_sum.size();
+  e->h_sum.resize(old + n);
+  HIPC(hipMemcpyAsync(e->h_sum.data() + old, e->sum, n * sizeof(gs_round_summary), hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  e->sum_used = 0;
+  return GS_OK;
+}
+
+int gs_record_round(gs_engine* eh) {
+  ENGINE(eh);
+  if (int s = need_slots(e)) return s;
+  hipEvent_t t0;
+  e->tbegin("stats", &t0);
+  hipError_t r = launch_stats(*e, e->sum_used);
+  e->tend("stats", t0);
+  HIPC(r);
+  if (++e->sum_used == e->sum_cap) return drain_summaries(e);
+  return GS_OK;
+}
+
+int gs_round(gs_engine* eh, uint32_t round, int record) {
+  ENGINE(eh);
+  if (int s = need_slots(e)) return s;
+  if (int s = do_bfs(e)) return s;
+  if (int s = do_cp(e, true, true, true)) return s;
+  if (int s = gs_chance_to_rotate(eh, round)) return s;
+  if (record) return gs_record_round(eh);
+  return GS_OK;
+}
+
+// ------------------------------------------------------------ readbacks ----
+#define SLOT_CHECK(slot) \
+  if ((slot) >= e->S) return fail(GS_EINVAL, "slot out of range");
+
+int gs_read_hops(gs_engine* eh, uint32_t slot, uint8_t* hops) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  if (int s = check_err(e)) return s;
+  HIPC(hipMemcpyAsync(hops, e->hops + (size_t)slot * e->N, e->N, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_read_inbound(gs_engine* eh, uint32_t slot, uint32_t* off, uint32_t* src, uint8_t* hop, size_t cap) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  if (int s = check_err(e)) return s;
+  const size_t N = e->N, base = (size_t)slot * N;
+  std::vector<uint32_t> cnt(N), recs(N * e->capin);
+  HIPC(hipMemcpyAsync(cnt.data(), e->cnt + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpy2DAsync(recs.data(), N * 4, e->inb + base, e->PAIRS * 4, N * 4, e->capin, hipMemcpyDeviceToHost,
+                        e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  size_t total = 0;
+  for (size_t v = 0; v < N; ++v) total += cnt[v];
+  if (total > cap) return fail(GS_ERANGE, "inbound buffer too small");
+  off[0] = 0;
+  size_t w = 0;
+  std::vector<uint32_t> lst;
+  for (size_t v = 0; v < N; ++v) {
+    lst.clear();
+    for (uint32_t j = 0; j < cnt[v]; ++j) lst.push_back(recs[(size_t)j * N + v]);
+    std::sort(lst.begin(), lst.end());
+    for (uint32_t r : lst) { src[w] = r & 0xFFFFFFu; hop[w] = (uint8_t)(r >> 24); ++w; }
+    off[v + 1] = (uint32_t)w;
+  }
+  return GS_OK;
+}
+
+// Copies the cache columns of one slot: keys/scores [CACHE_CAP][N].
+static int read_cache_slot(Engine* e, uint32_t slot, std::vector<uint32_t>& meta, std::vector<uint32_t>& keys,
+                           std::vector<uint8_t>& scores) {
+  const size_t N = e->N, base = (size_t)slot * N;
+  meta.resize(N); keys.resize(N * CACHE_CAP); scores.resize(N * CACHE_CAP);
+  HIPC(hipMemcpyAsync(meta.data(), e->cmeta + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpy2DAsync(keys.data(), N * 4, e->ckey + base, e->PAIRS * 4, N * 4, CACHE_CAP, hipMemcpyDeviceToHost,
+                        e->st));
+  HIPC(hipMemcpy2DAsync(scores.data(), N, e->cscore + base, e->PAIRS, N, CACHE_CAP, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_read_prunes(gs_engine* eh, uint32_t slot, uint32_t* pruner, uint32_t* prunee, size_t cap, size_t* count) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  if (int s = check_err(e)) return s;
+  std::vector<uint32_t> meta, keys;
+  std::vector<uint8_t> sc;
+  if (int s = read_cache_slot(e, slot, meta, keys, sc)) return s;
+  std::vector<std::pair<uint32_t, uint32_t>> pr;
+  const size_t N = e->N;
+  for (size_t v = 0; v < N; ++v) {
+    const uint32_t plen = (meta[v] >> 16) & 0xFF;
+    for (uint32_t i = 0; i < plen; ++i)
+      if (sc[i * N + v] & PRUNED_FLAG) pr.push_back({(uint32_t)v, keys[i * N + v]});
+  }
+  std::sort(pr.begin(), pr.end());
+  *count = pr.size();
+  if (pr.size() > cap) return fail(GS_ERANGE, "prunes buffer too small");
+  for (size_t i = 0; i < pr.size(); ++i) { pruner[i] = pr[i].first; prunee[i] = pr[i].second; }
+  return GS_OK;
+}
+
+int gs_read_cache(gs_engine* eh, uint32_t slot, uint32_t node, uint32_t* up, uint32_t* keys, uint32_t* scores,
+                  uint32_t cap, uint32_t* len) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  if (node >= e->N) return fail(GS_EINVAL, "node out of range");
+  if (int s = check_err(e)) return s;
+  const size_t p = (size_t)slot * e->N + node;
+  uint32_t meta = 0;
+  uint32_t* dk = nullptr;
+  uint8_t* ds = nullptr;
+  HIPC(hipMalloc(&dk, CACHE_CAP * 4));
+  HIPC(hipMalloc(&ds, CACHE_CAP));
+  HIPC(hipMemcpyAsync(&meta, e->cmeta + p, 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(launch_gather_strided_u32(*e, e->ckey + p, e->PAIRS, CACHE_CAP, dk));
+  HIPC(launch_gather_strided_u8(*e, e->cscore + p, e->PAIRS, CACHE_CAP, ds));
+  std::vector<uint32_t> k(CACHE_CAP);
+  std::vector<uint8_t> s(CACHE_CAP);
+  HIPC(hipMemcpyAsync(k.data(), dk, CACHE_CAP * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(s.data(), ds, CACHE_CAP, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  hipFree(dk);
+  hipFree(ds);
+  const uint32_t L = meta & 0xFF;
+  *up = (meta >> 8) & 0xFF;
+  *len = L;
+  if (L > cap) return fail(GS_ERANGE, "cache buffer too small");
+  std::vector<std::pair<uint32_t, uint32_t>> v;
+  for (uint32_t i = 0; i < L; ++i) v.push_back({k[i], (uint32_t)(s[i] & 0x7F)});
+  std::sort(v.begin(), v.end());
+  for (uint32_t i = 0; i < L; ++i) { keys[i] = v[i].first; scores[i] = v[i].second; }
+  return GS_OK;
+}
+
+int gs_read_pruned(gs_engine* eh, uint32_t slot, uint32_t node, uint32_t* fifo_mask) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  if (node >= e->N) return fail(GS_EINVAL, "node out of range");
+  if (int s = check_err(e)) return s;
+  uint32_t m = 0, org = e->slots[slot].origin;
+  uint8_t bn = 0, bo = 0;
+  HIPC(hipMemcpyAsync(&m, e->mask + (size_t)slot * e->N + node, 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(&bn, e->bucket + node, 1, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(&bo, e->bucket + org, 1, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  const size_t ent = (size_t)node * NB + std::min(bn, bo);
+  uint16_t hv = 0;
+  HIPC(hipMemcpy(&hv, e->hl + ent, 2, hipMemcpyDeviceToHost));
+  const uint32_t head = hv & 0xFF, L = hv >> 8;
+  uint32_t out = 0;
+  for (uint32_t j = 0; j < L; ++j)
+    if ((m >> ((head + j) % e->ASZ)) & 1u) out |= 1u << j;
+  *fifo_mask = out;
+  return GS_OK;
+}
+
+int gs_read_active_sets(gs_engine* eh, uint32_t* peers, uint8_t* len) {
+  ENGINE(eh);
+  if (int s = check_err(e)) return s;
+  const size_t ents = (size_t)e->N * NB;
+  std::vector<uint32_t> rows(ents * e->ASZP);
+  std::vector<uint16_t> hl(ents);
+  HIPC(hipMemcpyAsync(rows.data(), e->peers, rows.size() * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(hl.data(), e->hl, ents * 2, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  for (size_t ent = 0; ent < ents; ++ent) {
+    const uint32_t head = hl[ent] & 0xFF, L = hl[ent] >> 8;
+    len[ent] = (uint8_t)L;
+    for (uint32_t j = 0; j < e->ASZ; ++j)
+      peers[ent * e->ASZ + j] = j < L ? rows[ent * e->ASZP + (head + j) % e->ASZ] : 0xFFFFFFFFu;
+  }
+  return GS_OK;
+}
+
+int gs_read_caches(gs_engine* eh, uint32_t slot, uint32_t* up, uint32_t* len, uint32_t* keys, uint32_t* scores) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  if (int s = check_err(e)) return s;
+  std::vector<uint32_t> meta, k;
+  std::vector<uint8_t> sc;
+  if (int s = read_cache_slot(e, slot, meta, k, sc)) return s;
+  const size_t N = e->N;
+  std::vector<std::pair<uint32_t, uint32_t>> v;
+  for (size_t n = 0; n < N; ++n) {
+    const uint32_t L = meta[n] & 0xFF;
+    up[n] = (meta[n] >> 8) & 0xFF;
+    len[n] = L;
+    v.clear();
+    for (uint32_t i = 0; i < L; ++i) v.push_back({k[i * N + n], (uint32_t)(sc[i * N + n] & 0x7F)});
+    std::sort(v.begin(), v.end());
+    for (uint32_t i = 0; i < CACHE_CAP; ++i) {
+      keys[n * CACHE_CAP + i] = i < L ? v[i].first : 0xFFFFFFFFu;
+      scores[n * CACHE_CAP + i] = i < L ? v[i].second : 0;
+    }
+  }
+  return GS_OK;
+}
+
+int gs_read_pruned_all(gs_engine* eh, uint32_t slot, uint32_t* fifo_mask) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  if (int s = check_err(e)) return s;
+  const size_t N = e->N;
+  std::vector<uint32_t> m(N);
+  std::vector<uint8_t> b(N);
+  std::vector<uint16_t> hl(N * NB);
+  HIPC(hipMemcpyAsync(m.data(), e->mask + slot * N, N * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(b.data(), e->bucket, N, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(hl.data(), e->hl, N * NB * 2, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  const uint32_t bo = b[e->slots[slot].origin];
+  for (size_t n = 0; n < N; ++n) {
+    const uint16_t hv = hl[n * NB + std::min<uint32_t>(b[n], bo)];
+    const uint32_t head = hv & 0xFF, L = hv >> 8;
+    uint32_t out = 0;
+    for (uint32_t j = 0; j < L; ++j)
+      if ((m[n] >> ((head + j) % e->ASZ)) & 1u) out |= 1u << j;
+    fifo_mask[n] = out;
+  }
+  return GS_OK;
+}
+
+int gs_read_counters(gs_engine* eh, uint32_t slot, uint32_t* egress, uint32_t* ingress, uint32_t* prune_sent) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  if (int s = check_err(e)) return s;
+  const size_t N = e->N, base = (size_t)slot * N;
+  std::vector<uint8_t> eg(N), hp(N), pr(N);
+  HIPC(hipMemcpyAsync(eg.data(), e->egress + base, N, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(hp.data(), e->hops + base, N, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(pr.data(), e->prune_round + base, N, hipMemcpyDeviceToHost, e->st));
+  if (ingress) HIPC(hipMemcpyAsync(ingress, e->cnt + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  for (size_t v = 0; v < N; ++v) {
+    if (egress) egress[v] = hp[v] != 0xFF ? eg[v] : 0;
+    if (prune_sent) prune_sent[v] = pr[v];
+  }
+  return GS_OK;
+}
+
+int gs_read_round_summaries(gs_engine* eh, gs_round_summary* out, size_t cap, size_t* count) {
+  ENGINE(eh);
+  if (int s = check_err(e)) return s;
+  if (int s = drain_summaries(e)) return s;
+  *count = e->h_sum.size();
+  if (e->h_sum.size() > cap) return fail(GS_ERANGE, "summary buffer too small");
+  std::memcpy(out, e->h_sum.data(), e->h_sum.size() * sizeof(gs_round_summary));
+  return GS_OK;
+}
+
+int gs_read_accumulators(gs_engine* eh, uint32_t slot, uint64_t* egress, uint64_t* ingress, uint64_t* prunes,
+                         uint32_t* stranded_times, uint64_t* hop_hist) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  if (int s = check_err(e)) return s;
+  const size_t N = e->N, base = (size_t)slot * N;
+  std::vector<uint32_t> a(N), b(N), c(N);
+  HIPC(hipMemcpyAsync(a.data(), e->egress_acc + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(b.data(), e->ingress_acc + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(c.data(), e->prune_acc + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  if (stranded_times) HIPC(hipMemcpyAsync(stranded_times, e->strand + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  if (hop_hist) HIPC(hipMemcpyAsync(hop_hist, e->hist_acc + (size_t)slot * 256, 256 * 8, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  for (size_t v = 0; v < N; ++v) {
+    if (egress) egress[v] = a[v];
+    if (ingress) ingress[v] = b[v];
+    if (prunes) prunes[v] = c[v];
+  }
+  return GS_OK;
+}
+
+int gs_read_failed(gs_engine* eh, uint32_t slot, uint8_t* failed) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  std::vector<uint32_t> fr(e->N);
+  uint32_t nf = 0;
+  HIPC(hipMemcpyAsync(fr.data(), e->frank, e->N * 4ull, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(&nf, e->nfail + slot, 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  for (uint32_t v = 0; v < e->N; ++v) failed[v] = nf && fr[v] < nf;
+  return GS_OK;
+}
+
+int gs_kernel_time(gs_engine* eh, const char* family, double* ms, uint64_t* launches) {
+  ENGINE(eh);
+  HIPC(hipStreamSynchronize(e->st));
+  auto it = e->timers.find(family ? family : "");
+  *ms = 0;
+  *launches = 0;
+  if (it == e->timers.end()) return GS_OK;
+  auto& t = it->second;
+  for (auto& pr : t.ev) {
+    float x = 0;
+    hipEventElapsedTime(&x, pr.first, pr.second);
+    t.ms += x;
+    t.n += 1;
+    hipEventDestroy(pr.first);
+    hipEventDestroy(pr.second);
+  }
+  t.ev.clear();
+  *ms = t.ms;
+  *launches = t.n;
+  return GS_OK;
+}
+
+int gs_kernel_time_reset(gs_engine* eh) {
+  ENGINE(eh);
+  HIPC(hipStreamSynchronize(e->st));
+  for (auto& kv : e->timers) {
+    for (auto& pr : kv.second.ev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+    kv.second.ev.clear();
+    kv.second.ms = 0;
+    kv.second.n = 0;
+  }
+  return GS_OK;
+}
+
+int gs_engine_info(gs_engine* eh, uint32_t* n_nodes, uint32_t* n_slots, uint32_t* bfs_mode, uint64_t* bytes) {
+  Engine* e = reinterpret_cast<Engine*>(eh);
+  if (!e) return fail(GS_EINVAL, "null engine");
+  if (n_nodes) *n_nodes = e->N;
+  if (n_slots) *n_slots = e->S;
+  if (bfs_mode) *bfs_mode = e->bfs_mode;
+  if (bytes) *bytes = e->dev_bytes;
+  return GS_OK;
+}
+
+}  // extern "C"

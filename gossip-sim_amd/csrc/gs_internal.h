@@ -1,0 +1,106 @@
+// gs_internal.h -- engine state shared by the kernels' launchers and the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/gossip_hip.h"
+
+namespace gs {
+
+// Device-resident state. Layout (DESIGN.md "Data layout in HBM"):
+//  per node      stake u64, bucket u8, fail rank u32, stake rank u32
+//  per (node,k)  peers[ASZP] u32 ring + hl u16 (head | len << 8)      -- PushActiveSet
+//  per k         prefix sums of rotation weights P[k][N+1] u64
+//  per pair      (slot-major pair p = slot * N + node)
+//                hops u8, in-degree u32, prune mask u32 (bits = physical ring slots),
+//                inbound records u32 [capin][pairs] (hop << 24 | src),
+//                cache meta u32 (len | upserts << 8 | pruned-len << 16),
+//                cache keys u32 [96][pairs], scores u8 [96][pairs] (bit 7 = pruned),
+//                egress/prune-sent of the round u8, measured accumulators u32
+struct Engine {
+  gs_params prm{};
+  uint32_t N = 0, S = 0;
+  size_t PAIRS = 0;
+  uint32_t ASZ = 0, ASZP = 0, fanout = 0, capin = 64;
+  uint32_t bfs_mode = GS_BFS_LEVEL;
+  hipStream_t st = nullptr;
+  size_t dev_bytes = 0;
+  std::vector<void*> allocs;
+
+  // node arrays
+  uint64_t* stake = nullptr;
+  uint8_t* bucket = nullptr;
+  uint64_t* P = nullptr;
+  uint32_t* peers = nullptr;
+  uint16_t* hl = nullptr;
+  uint32_t* frank = nullptr;
+  uint32_t* srank = nullptr;
+  uint32_t* by_srank = nullptr;
+  // slot arrays
+  uint32_t* origin = nullptr;
+  uint8_t* obkt = nullptr;
+  uint32_t* min_ingress = nullptr;
+  double* thr = nullptr;
+  uint32_t* nfail = nullptr;
+  uint32_t* slot_prunes = nullptr;  // prunees emitted in the current round
+  // pair arrays
+  uint8_t* hops = nullptr;
+  uint32_t* cnt = nullptr;
+  uint32_t* mask = nullptr;
+  uint32_t* inb = nullptr;
+  uint32_t* cmeta = nullptr;
+  uint32_t* ckey = nullptr;
+  uint8_t* cscore = nullptr;
+  uint8_t* egress = nullptr;
+  uint8_t* prune_round = nullptr;
+  uint32_t* egress_acc = nullptr;
+  uint32_t* ingress_acc = nullptr;
+  uint32_t* prune_acc = nullptr;
+  uint32_t* strand = nullptr;
+  // level-synchronous BFS
+  uint32_t* q[2] = {nullptr, nullptr};
+  uint32_t* lvl = nullptr;  // frontier sizes per level [256]
+  // rotation
+  uint32_t* rot_list = nullptr;
+  uint32_t* rot_count = nullptr;
+  uint32_t* rot_changed = nullptr;
+  // stats
+  uint32_t* rs_u32 = nullptr;   // per slot: visited, pushes, stranded, pad
+  uint64_t* rs_ssum = nullptr;  // per slot: stranded stake sum
+  uint32_t* rs_hist = nullptr;  // per slot: 256 hop bins of this round
+  uint64_t* hist_acc = nullptr; // per slot: 256 hop bins over recorded rounds
+  uint32_t* bm = nullptr;       // per slot: stranded bitmap over stake rank
+  uint32_t bm_words = 0;
+  gs_round_summary* sum = nullptr;  // device ring of recorded summaries [sum_cap][S]
+  uint32_t sum_cap = 0, sum_used = 0;
+  std::vector<gs_round_summary> h_sum;  // drained summaries
+  uint32_t* err = nullptr;
+  uint32_t* h_err = nullptr;  // pinned
+
+  std::vector<gs_slot> slots;
+  bool slots_set = false, failed_ranked = false;
+
+  // profiling
+  struct Timed { std::vector<std::pair<hipEvent_t, hipEvent_t>> ev; double ms = 0; uint64_t n = 0; };
+  std::map<std::string, Timed> timers;
+  void tbegin(const char* fam, hipEvent_t* a);
+  void tend(const char* fam, hipEvent_t a);
+};
+
+// launchers (gs_kernels.hip); all enqueue on e.st and return hipError_t
+hipError_t launch_prefix_weights(Engine& e);
+hipError_t launch_init_entries(Engine& e);
+hipError_t launch_fail_keys(Engine& e, uint64_t* keys, uint32_t* ids);
+hipError_t launch_scatter_rank(Engine& e, const uint32_t* sorted_ids, uint32_t* rank_out);
+hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket, uint32_t bits);
+hipError_t launch_bfs(Engine& e);
+hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply);
+hipError_t launch_rotate(Engine& e, uint32_t round);
+hipError_t launch_stats(Engine& e, uint32_t rec_index);
+hipError_t launch_gather_strided_u32(Engine& e, const uint32_t* src, size_t stride, uint32_t n, uint32_t* dst);
+hipError_t launch_gather_strided_u8(Engine& e, const uint8_t* src, size_t stride, uint32_t n, uint8_t* dst);
+
+}  // namespace gs

@@ -1,0 +1,848 @@
+// gs_kernels.hip -- gfx950 kernels of the push-propagation engine.
+//
+// Kernel map (reference function each one restates):
+//   k_prefix_weights   rotation weights (push_active_set.rs:97-111) as prefix sums
+//   k_init_entries     PushActiveSet::rotate on empty entries (push_active_set.rs:73-114,153-187)
+//   k_rotate_*         Cluster::chance_to_rotate -> Node::rotate_active_set (gossip.rs:739-754,815-842)
+//   k_bfs_wg           Cluster::run_gossip (gossip.rs:494-615), one workgroup per slot, LDS frontier
+//   k_bfs_level        Cluster::run_gossip, level-synchronous over all slots (large N)
+//   k_consume_prune    consume_messages + ReceivedCache::record/prune + send_prunes +
+//                      prune_connections (gossip.rs:618-737, received_cache.rs:27-131)
+//   k_stats_*          the measured-round statistics inserts (gossip_main.rs:480-563)
+#include <hipcub/hipcub.hpp>
+
+#include "gs_device.h"
+#include "gs_internal.h"
+
+namespace gs {
+
+static inline uint32_t grid_for(size_t n, uint32_t block, uint32_t cap = 1u << 20) {
+  size_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (uint32_t)g;
+}
+
+// -------------------------------------------------------------- weights ----
+__global__ __launch_bounds__(1024) void k_prefix_weights(const uint8_t* __restrict__ bucket, uint64_t* __restrict__ P,
+                                                        uint32_t N) {
+  const int k = blockIdx.x;
+  uint64_t* Pk = P + (size_t)k * (N + 1);
+  const uint32_t T = blockDim.x, t = threadIdx.x;
+  const uint32_t chunk = (N + T - 1) / T;
+  const uint32_t lo = min(N, t * chunk), hi = min(N, lo + chunk);
+  uint64_t s = 0;
+  for (uint32_t i = lo; i < hi; ++i) s += weight(k, bucket[i]);
+  __shared__ uint64_t part[1024];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < T; off <<= 1) {
+    uint64_t v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint64_t run = part[t] - s;
+  if (t == 0) Pk[0] = 0;
+  for (uint32_t i = lo; i < hi; ++i) {
+    run += weight(k, bucket[i]);
+    Pk[i + 1] = run;
+  }
+}
+
+hipError_t launch_prefix_weights(Engine& e) {
+  hipLaunchKernelGGL(k_prefix_weights, dim3(NB), dim3(1024), 0, e.st, e.bucket, e.P, e.N);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------ init (R6) ----
+// One thread per entry (u, k). From an empty entry the reference appends fresh
+// shuffle draws until len > size, then drops the oldest: the entry keeps draws
+// 2..size+1 (or every candidate when N - 1 <= size).
+template <int ASZP>
+__global__ __launch_bounds__(256) void k_init_entries(const uint8_t* __restrict__ bucket,
+                                                     const uint64_t* __restrict__ P, uint32_t* __restrict__ peers,
+                                                     uint16_t* __restrict__ hl, uint32_t N, uint32_t size,
+                                                     uint64_t seed) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= N * NB) return;
+  const uint32_t u = gid / NB, k = gid % NB;
+  const uint64_t* Pk = P + (size_t)k * (N + 1);
+  constexpr int R = ASZP + 2;
+  uint32_t rem[R];
+  uint64_t remw[R];
+  int nr = 0;
+  const uint64_t wself = weight(k, bucket[u]);
+  rem_insert(rem, remw, nr, u, wself);
+  uint64_t left = Pk[N] - wself;
+  const uint32_t ncand = N - 1;
+  const uint32_t T = min(ncand, size + 1);
+  const bool drop = ncand >= size + 1;
+  Philox s(seed, P_INIT, u, k);
+  uint32_t* row = peers + (size_t)gid * ASZP;
+  uint32_t filled = 0;
+  for (uint32_t t = 0; t < T; ++t) {
+    const uint64_t v = sample_below(left, s);
+    const uint32_t c = shuffle_pick(Pk, N, v, rem, remw, nr);
+    const uint64_t wc = weight(k, bucket[c]);
+    left -= wc;
+    rem_insert(rem, remw, nr, c, wc);
+    if (!(t == 0 && drop)) row[filled++] = c;
+  }
+  hl[gid] = (uint16_t)(filled << 8);
+}
+
+#define GS_ASZP_DISPATCH(ASZP_VAL, CALL)          \
+  switch (ASZP_VAL) {                             \
+    case 4: { constexpr int A = 4; CALL; } break; \
+    case 8: { constexpr int A = 8; CALL; } break; \
+    case 12: { constexpr int A = 12; CALL; } break; \
+    case 16: { constexpr int A = 16; CALL; } break; \
+    case 20: { constexpr int A = 20; CALL; } break; \
+    case 24: { constexpr int A = 24; CALL; } break; \
+    case 28: { constexpr int A = 28; CALL; } break; \
+    case 32: { constexpr int A = 32; CALL; } break; \
+    default: return hipErrorInvalidValue;         \
+  }
+
+hipError_t launch_init_entries(Engine& e) {
+  const uint32_t total = e.N * NB;
+  GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_init_entries<A>, dim3(grid_for(total, 256)), dim3(256), 0, e.st,
+                                              e.bucket, e.P, e.peers, e.hl, e.N, e.ASZ, e.prm.seed));
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------ fail (R15) ----
+__global__ void k_fail_keys(uint32_t N, uint64_t seed, uint64_t* keys, uint32_t* ids) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= N) return;
+  Philox s(seed, P_FAIL, v, 0);
+  keys[v] = s.next();
+  ids[v] = v;
+}
+hipError_t launch_fail_keys(Engine& e, uint64_t* keys, uint32_t* ids) {
+  hipLaunchKernelGGL(k_fail_keys, dim3(grid_for(e.N, 256)), dim3(256), 0, e.st, e.N, e.prm.seed, keys, ids);
+  return hipGetLastError();
+}
+__global__ void k_scatter_rank(uint32_t N, const uint32_t* sorted_ids, uint32_t* rank) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < N) rank[sorted_ids[i]] = i;
+}
+hipError_t launch_scatter_rank(Engine& e, const uint32_t* sorted_ids, uint32_t* rank_out) {
+  hipLaunchKernelGGL(k_scatter_rank, dim3(grid_for(e.N, 256)), dim3(256), 0, e.st, e.N, sorted_ids, rank_out);
+  return hipGetLastError();
+}
+
+__global__ void k_clear_slot_masks(uint32_t N, uint32_t S, uint32_t node, uint32_t bucket_k,
+                                   const uint8_t* __restrict__ bucket, const uint8_t* __restrict__ obkt,
+                                   uint32_t bits, uint32_t* mask) {
+  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= S) return;
+  const uint32_t b = min((uint32_t)bucket[node], (uint32_t)obkt[o]);
+  if (b == bucket_k) mask[(size_t)o * N + node] &= ~bits;
+}
+hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket_k, uint32_t bits) {
+  hipLaunchKernelGGL(k_clear_slot_masks, dim3(grid_for(e.S, 256)), dim3(256), 0, e.st, e.N, e.S, node, bucket_k,
+                     e.bucket, e.obkt, bits, e.mask);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------- rotation (R14) ----
+__global__ void k_rotate_decide(uint32_t N, uint64_t seed, uint32_t round, double p, uint32_t* rot_list,
+                                uint32_t* rot_count) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= N) return;
+  Philox s(seed, P_DECIDE, u, round);
+  if (unit_f64(s.next()) < p) rot_list[atomicAdd(rot_count, 1u)] = u;
+}
+
+// One thread per (rotating node, entry k). On a full entry the reference's loop
+// appends the first drawn peer that is not present, draws once more and breaks,
+// then drops the oldest: the ring's head slot is overwritten.
+template <int ASZP>
+__global__ __launch_bounds__(256) void k_rotate_entries(const uint8_t* __restrict__ bucket,
+                                                       const uint64_t* __restrict__ P, uint32_t* __restrict__ peers,
+                                                       uint16_t* __restrict__ hl, const uint32_t* __restrict__ rot_list,
+                                                       const uint32_t* __restrict__ rot_count,
+                                                       uint32_t* __restrict__ rot_changed, uint32_t N, uint32_t size,
+                                                       uint64_t seed, uint32_t round) {
+  const uint32_t total = *rot_count * NB;
+  for (uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x; gid < total; gid += gridDim.x * blockDim.x) {
+    const uint32_t i = gid / NB, k = gid % NB;
+    const uint32_t u = rot_list[i];
+    const uint32_t ent = u * NB + k;
+    const uint16_t hv = hl[ent];
+    uint32_t head = hv & 0xFF, L = hv >> 8;
+    const uint32_t S = size;
+    uint32_t* row = peers + (size_t)ent * ASZP;
+    const uint64_t* Pk = P + (size_t)k * (N + 1);
+    constexpr int R = ASZP + 2;
+    uint32_t rem[R];
+    uint64_t remw[R];
+    int nr = 0;
+    const uint64_t wself = weight(k, bucket[u]);
+    rem_insert(rem, remw, nr, u, wself);
+    uint64_t left = Pk[N] - wself;
+    Philox s(seed, P_ROTATE, u, (round << 5) | k);
+    uint32_t changed = 0;
+    for (uint32_t drawn = 0; drawn + 1 < N; ++drawn) {
+      const uint64_t v = sample_below(left, s);
+      const uint32_t c = shuffle_pick(Pk, N, v, rem, remw, nr);
+      const uint64_t wc = weight(k, bucket[c]);
+      left -= wc;
+      if (nr < R) rem_insert(rem, remw, nr, c, wc);
+      bool present = false;
+      for (uint32_t j = 0; j < L; ++j) {
+        uint32_t slot = head + j;
+        if (slot >= S) slot -= S;
+        present |= row[slot] == c;
+      }
+      if (present) continue;
+      if (L < S) {
+        uint32_t slot = head + L;
+        if (slot >= S) slot -= S;
+        row[slot] = c;
+        ++L;
+        changed |= 1u << slot;
+        continue;
+      }
+      row[head] = c;
+      changed |= 1u << head;
+      head = head + 1 == S ? 0 : head + 1;
+      break;
+    }
+    hl[ent] = (uint16_t)((L << 8) | head);
+    rot_changed[gid] = changed;
+  }
+}
+
+// A replaced peer gets a fresh filter: clear its ring slot's prune bit for every
+// slot whose origin uses that entry.
+__global__ void k_rotate_clear(uint32_t N, uint32_t S, const uint8_t* __restrict__ bucket,
+                               const uint8_t* __restrict__ obkt, const uint32_t* __restrict__ rot_list,
+                               const uint32_t* __restrict__ rot_count, const uint32_t* __restrict__ rot_changed,
+                               uint32_t* __restrict__ mask) {
+  const uint32_t total = *rot_count * S;
+  for (uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x; gid < total; gid += gridDim.x * blockDim.x) {
+    const uint32_t i = gid / S, o = gid - i * S;
+    const uint32_t u = rot_list[i];
+    const uint32_t b = min((uint32_t)bucket[u], (uint32_t)obkt[o]);
+    const uint32_t m = rot_changed[i * NB + b];
+    if (m) mask[(size_t)o * N + u] &= ~m;
+  }
+}
+
+hipError_t launch_rotate(Engine& e, uint32_t round) {
+  hipError_t r = hipMemsetAsync(e.rot_count, 0, sizeof(uint32_t), e.st);
+  if (r != hipSuccess) return r;
+  hipLaunchKernelGGL(k_rotate_decide, dim3(grid_for(e.N, 256)), dim3(256), 0, e.st, e.N, e.prm.seed, round,
+                     e.prm.rotation_probability, e.rot_list, e.rot_count);
+  GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_rotate_entries<A>, dim3(grid_for((size_t)e.N * NB, 256, 2048)),
+                                              dim3(256), 0, e.st, e.bucket, e.P, e.peers, e.hl, e.rot_list,
+                                              e.rot_count, e.rot_changed, e.N, e.ASZ, e.prm.seed, round));
+  hipLaunchKernelGGL(k_rotate_clear, dim3(grid_for((size_t)e.N * e.S, 256, 2048)), dim3(256), 0, e.st, e.N, e.S,
+                     e.bucket, e.obkt, e.rot_list, e.rot_count, e.rot_changed, e.mask);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------- BFS (R8) ----
+struct BfsArgs {
+  const uint8_t* bucket;
+  const uint32_t* peers;
+  const uint16_t* hl;
+  const uint32_t* frank;
+  const uint32_t* origin;
+  const uint8_t* obkt;
+  const uint32_t* nfail;
+  const uint32_t* mask;
+  uint8_t* hops;
+  uint32_t* cnt;
+  uint32_t* inb;
+  uint8_t* egress;
+  uint32_t* lvl;
+  uint32_t* err;
+  uint32_t N, S, ASZ, fanout, capin;
+  size_t PAIRS;
+};
+
+template <int ASZP>
+__device__ inline void load_row(const uint32_t* __restrict__ src, uint32_t (&row)[ASZP]) {
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+  for (int q = 0; q < ASZP / 4; ++q) {
+    const uint4 x = s4[q];
+    row[4 * q] = x.x; row[4 * q + 1] = x.y; row[4 * q + 2] = x.z; row[4 * q + 3] = x.w;
+  }
+}
+
+// PushActiveSet::get_nodes(..).take(fanout) (gossip.rs:527-536, push_active_set.rs:128-141):
+// the first `fanout` peers in FIFO order whose filter lacks the origin -- i.e.
+// not pruned for this slot and not the origin itself. Returns physical ring slots.
+template <int ASZP>
+__device__ inline uint32_t taken_slots(const uint32_t (&row)[ASZP], uint32_t head, uint32_t len, uint32_t S,
+                                       uint32_t pmask, uint32_t origin, uint32_t fanout) {
+  uint32_t elig = 0;
+#pragma unroll
+  for (int s = 0; s < ASZP; ++s) {
+    const uint32_t pos = (uint32_t)s >= head ? (uint32_t)s - head : (uint32_t)s + S - head;
+    const bool ok = (uint32_t)s < S && pos < len && !((pmask >> s) & 1u) && row[s] != origin;
+    elig |= (uint32_t)ok << s;
+  }
+  const uint64_t full = (S == 64) ? ~0ull : ((1ull << S) - 1);
+  const uint64_t e64 = elig;
+  uint64_t fifo = ((e64 >> head) | (e64 << (S - head))) & full;
+  if ((uint32_t)__popcll(fifo) > fanout) {
+    uint64_t sel = 0;
+    for (uint32_t t = 0; t < fanout; ++t) {
+      const uint64_t low = fifo & (~fifo + 1);
+      sel |= low;
+      fifo ^= low;
+    }
+    fifo = sel;
+  }
+  return (uint32_t)(((fifo << head) | (fifo >> (S - head))) & full);
+}
+
+__device__ inline uint32_t lane_id() { return __lane_id(); }
+
+// Workgroup-per-slot BFS: hop table, in-degree counters and both frontier
+// queues live in LDS (9 bytes per node), so the whole level loop runs with
+// workgroup barriers only. First visit = the in-degree atomic returning 0.
+template <int ASZP>
+__global__ __launch_bounds__(256) void k_bfs_wg(BfsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t N = a.N;
+  uint32_t* ctrl = reinterpret_cast<uint32_t*>(smem);  // [0] frontier size, [1] next size, [2] err
+  uint32_t* cnt_l = ctrl + 4;
+  uint8_t* hops_l = reinterpret_cast<uint8_t*>(cnt_l + N);
+  uint16_t* q0 = reinterpret_cast<uint16_t*>(hops_l + ((N + 3) & ~3u));
+  uint16_t* q1 = q0 + ((N + 1) & ~1u);
+  const uint32_t tid = threadIdx.x, bd = blockDim.x;
+  for (uint32_t o = blockIdx.x; o < a.S; o += gridDim.x) {
+    const uint32_t org = a.origin[o];
+    const uint32_t ob = a.obkt[o];
+    const uint32_t nf = a.nfail[o];
+    const size_t base = (size_t)o * N;
+    for (uint32_t v = tid; v < N; v += bd) { cnt_l[v] = 0; hops_l[v] = 0xFF; }
+    __syncthreads();
+    if (tid == 0) { ctrl[0] = 1; ctrl[1] = 0; ctrl[2] = 0; hops_l[org] = 0; q0[0] = (uint16_t)org; }
+    __syncthreads();
+    uint16_t* cur = q0;
+    uint16_t* nxt = q1;
+    for (uint32_t d = 0;; ++d) {
+      const uint32_t qn = ctrl[0];
+      if (qn == 0) break;
+      if (d + 1 >= 255) { if (tid == 0) atomicOr(a.err, ERR_DEPTH); break; }
+      const uint32_t rec_hop = (d + 1) << 24;
+      for (uint32_t i = tid; i < qn; i += bd) {
+        const uint32_t u = cur[i];
+        const uint32_t b = min((uint32_t)a.bucket[u], ob);
+        const uint32_t ent = u * NB + b;
+        const uint32_t hv = a.hl[ent];
+        uint32_t row[ASZP];
+        load_row<ASZP>(a.peers + (size_t)ent * ASZP, row);
+        const uint32_t phys = taken_slots<ASZP>(row, hv & 0xFF, hv >> 8, a.ASZ, a.mask[base + u], org, a.fanout);
+        uint32_t pushes = 0;
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s) {
+          const uint32_t peer = row[s];
+          bool push = (phys >> s) & 1u;
+          if (push && nf) push = a.frank[peer] >= nf;  // failed peers burn the fanout slot (gossip.rs:538-541)
+          bool is_new = false;
+          if (push) {
+            const uint32_t old = atomicAdd(&cnt_l[peer], 1u);
+            if (old < a.capin) a.inb[(size_t)old * a.PAIRS + base + peer] = rec_hop | u;
+            else ctrl[2] = 1;
+            is_new = old == 0;
+            if (is_new) hops_l[peer] = (uint8_t)(d + 1);
+            ++pushes;
+          }
+          const unsigned long long bal = __ballot(is_new);
+          if (bal) {
+            const int leader = __ffsll((long long)bal) - 1;
+            uint32_t qb = 0;
+            if ((int)lane_id() == leader) qb = atomicAdd(&ctrl[1], (uint32_t)__popcll(bal));
+            qb = __shfl(qb, leader);
+            if (is_new) nxt[qb + __popcll(bal & ((1ull << lane_id()) - 1))] = (uint16_t)peer;
+          }
+        }
+        a.egress[base + u] = (uint8_t)pushes;
+      }
+      __syncthreads();
+      if (tid == 0) { ctrl[0] = ctrl[1]; ctrl[1] = 0; }
+      uint16_t* t = cur; cur = nxt; nxt = t;
+      __syncthreads();
+    }
+    for (uint32_t v = tid; v < N; v += bd) {
+      a.hops[base + v] = hops_l[v];
+      a.cnt[base + v] = cnt_l[v];
+    }
+    if (tid == 0 && ctrl[2]) atomicOr(a.err, ERR_INBOUND);
+    __syncthreads();
+  }
+}
+
+__global__ void k_bfs_seed(BfsArgs a, uint32_t* q0) {
+  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= a.S) return;
+  const size_t p = (size_t)o * a.N + a.origin[o];
+  a.hops[p] = 0;
+  q0[o] = (uint32_t)p;
+  if (o == 0) a.lvl[0] = a.S;
+}
+
+// Level-synchronous BFS over every slot at once (frontier of pair indices).
+template <int ASZP>
+__global__ __launch_bounds__(256) void k_bfs_level(BfsArgs a, uint32_t d, const uint32_t* __restrict__ qcur,
+                                                  uint32_t* __restrict__ qnxt) {
+  const uint32_t qn = a.lvl[d];
+  const uint32_t N = a.N;
+  const uint32_t rec_hop = (d + 1) << 24;
+  bool overflow = false;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < qn; i += gridDim.x * blockDim.x) {
+    const uint32_t p = qcur[i];
+    const uint32_t o = p / N;
+    const uint32_t u = p - o * N;
+    const size_t base = (size_t)o * N;
+    const uint32_t org = a.origin[o];
+    const uint32_t nf = a.nfail[o];
+    const uint32_t b = min((uint32_t)a.bucket[u], (uint32_t)a.obkt[o]);
+    const uint32_t ent = u * NB + b;
+    const uint32_t hv = a.hl[ent];
+    uint32_t row[ASZP];
+    load_row<ASZP>(a.peers + (size_t)ent * ASZP, row);
+    const uint32_t phys = taken_slots<ASZP>(row, hv & 0xFF, hv >> 8, a.ASZ, a.mask[p], org, a.fanout);
+    uint32_t pushes = 0;
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) {
+      const uint32_t peer = row[s];
+      bool push = (phys >> s) & 1u;
+      if (push && nf) push = a.frank[peer] >= nf;
+      bool is_new = false;
+      if (push) {
+        const uint32_t old = atomicAdd(&a.cnt[base + peer], 1u);
+        if (old < a.capin) a.inb[(size_t)old * a.PAIRS + base + peer] = rec_hop | u;
+        else overflow = true;
+        is_new = old == 0;
+        if (is_new) a.hops[base + peer] = (uint8_t)(d + 1);
+        ++pushes;
+      }
+      const unsigned long long bal = __ballot(is_new);
+      if (bal) {
+        const int leader = __ffsll((long long)bal) - 1;
+        uint32_t qb = 0;
+        if ((int)lane_id() == leader) qb = atomicAdd(&a.lvl[d + 1], (uint32_t)__popcll(bal));
+        qb = __shfl(qb, leader);
+        if (is_new) qnxt[qb + __popcll(bal & ((1ull << lane_id()) - 1))] = (uint32_t)(base + peer);
+      }
+    }
+    a.egress[p] = (uint8_t)pushes;
+  }
+  if (overflow) atomicOr(a.err, ERR_INBOUND);
+}
+
+static BfsArgs bfs_args(Engine& e) {
+  BfsArgs a;
+  a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.frank = e.frank; a.origin = e.origin; a.obkt = e.obkt;
+  a.nfail = e.nfail; a.mask = e.mask; a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb; a.egress = e.egress;
+  a.lvl = e.lvl; a.err = e.err; a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin;
+  a.PAIRS = e.PAIRS;
+  return a;
+}
+
+size_t bfs_wg_lds_bytes(uint32_t N) {
+  return 16 + 4 * (size_t)N + ((N + 3) & ~3u) + 2 * 2 * (size_t)((N + 1) & ~1u);
+}
+
+hipError_t launch_bfs(Engine& e) {
+  BfsArgs a = bfs_args(e);
+  hipError_t r;
+  if (e.bfs_mode == GS_BFS_WORKGROUP) {
+    const size_t lds = bfs_wg_lds_bytes(e.N);
+    const uint32_t grid = e.S < 4096 ? e.S : 4096;
+    GS_ASZP_DISPATCH(e.ASZP, {
+      r = hipFuncSetAttribute((const void*)k_bfs_wg<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (r != hipSuccess) return r;
+      hipLaunchKernelGGL(k_bfs_wg<A>, dim3(grid), dim3(256), lds, e.st, a);
+    });
+    return hipGetLastError();
+  }
+  if ((r = hipMemsetAsync(e.hops, 0xFF, e.PAIRS, e.st)) != hipSuccess) return r;
+  if ((r = hipMemsetAsync(e.cnt, 0, e.PAIRS * 4, e.st)) != hipSuccess) return r;
+  if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st)) != hipSuccess) return r;
+  hipLaunchKernelGGL(k_bfs_seed, dim3(grid_for(e.S, 256)), dim3(256), 0, e.st, a, e.q[0]);
+  const uint32_t grid = grid_for(e.PAIRS, 256, 2048);
+  for (uint32_t d = 0; d < 254; ++d) {
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_bfs_level<A>, dim3(grid), dim3(256), 0, e.st, a, d, e.q[d & 1],
+                                                e.q[(d + 1) & 1]));
+    if ((d & 3) == 3) {  // poll the frontier size every 4 levels
+      uint32_t* h = e.h_err + 1;
+      if ((r = hipMemcpyAsync(h, e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st)) != hipSuccess) return r;
+      if ((r = hipStreamSynchronize(e.st)) != hipSuccess) return r;
+      if (*h == 0) return hipGetLastError();
+    }
+  }
+  return hipErrorNotSupported;  // frontier still non-empty after 254 levels: hop counts no longer fit u8
+}
+
+// --------------------------------------------- consume / prune (R9-R13) ----
+struct CpArgs {
+  const uint64_t* stake;
+  const uint8_t* bucket;
+  const uint32_t* peers;
+  const uint16_t* hl;
+  const uint32_t* origin;
+  const uint8_t* obkt;
+  const uint32_t* min_ingress;
+  const double* thr;
+  const uint32_t* cnt;
+  const uint32_t* inb;
+  uint32_t* cmeta;
+  uint32_t* ckey;
+  uint8_t* cscore;
+  uint8_t* prune_round;
+  uint32_t* slot_prunes;
+  uint32_t* mask;
+  uint32_t* err;
+  uint32_t N, S, ASZ, ASZP, capin;
+  size_t PAIRS;
+};
+
+// u64 -> f64 -> u64 of received_cache.rs:114, saturating like Rust's `as u64`.
+__device__ inline uint64_t min_ingress_stake(uint64_t stake, double thr) {
+  const double x = (double)stake * thr;
+  if (!(x > 0.0)) return 0;
+  if (x >= 18446744073709551616.0) return ~0ull;
+  return (uint64_t)x;
+}
+
+template <bool CONSUME, bool PRUNE, bool APPLY>
+__global__ __launch_bounds__(256) void k_consume_prune(CpArgs a) {
+  const size_t PAIRS = a.PAIRS;
+  bool cache_overflow = false;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < PAIRS; p += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t o = (uint32_t)(p / a.N);
+    const uint32_t v = (uint32_t)(p - (size_t)o * a.N);
+    uint32_t meta = a.cmeta[p];
+    uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
+    if (CONSUME) {
+      // consume_messages (gossip.rs:618-653): inbound sorted by (hop, base58 id) =
+      // ascending record value; ReceivedCache::record with num_dups = rank.
+      uint32_t c = a.cnt[p];
+      if (c > a.capin) c = a.capin;
+      if (c) {
+        uint32_t prev = 0;
+        for (uint32_t k = 0; k < c; ++k) {
+          uint32_t best = 0xFFFFFFFFu;
+          for (uint32_t j = 0; j < c; ++j) {
+            const uint32_t r = a.inb[(size_t)j * PAIRS + p];
+            if ((k == 0 || r > prev) && r < best) best = r;
+          }
+          prev = best;
+          const uint32_t src = best & 0xFFFFFFu;
+          if (k == 0) up = up < 255 ? up + 1 : 255;
+          int found = -1;
+          for (uint32_t i = 0; i < len; ++i)
+            if (a.ckey[(size_t)i * PAIRS + p] == src) { found = (int)i; break; }
+          if (k < 2) {
+            if (found >= 0) {
+              uint8_t& sc = a.cscore[(size_t)found * PAIRS + p];
+              const uint32_t s0 = sc & 0x7F;
+              sc = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
+            } else if (len < CACHE_CAP) {
+              a.ckey[(size_t)len * PAIRS + p] = src;
+              a.cscore[(size_t)len * PAIRS + p] = 1;
+              ++len;
+            } else {
+              cache_overflow = true;
+            }
+          } else if (found < 0 && len < CACHE_LIMIT) {
+            a.ckey[(size_t)len * PAIRS + p] = src;
+            a.cscore[(size_t)len * PAIRS + p] = 0;
+            ++len;
+          }
+        }
+      }
+      meta = len | (up << 8) | (meta & 0xFF0000u);
+    }
+    uint32_t plen = (meta >> 16) & 0xFF;
+    if (PRUNE) {
+      // send_prunes -> ReceivedCache::prune (received_cache.rs:38-63,100-131).
+      uint32_t npr = 0;
+      plen = 0;
+      if (up >= MIN_NUM_UPSERTS) {
+        const uint32_t org = a.origin[o];
+        const uint64_t sv = a.stake[v], so = a.stake[org];
+        const uint64_t mis = min_ingress_stake(sv < so ? sv : so, a.thr[o]);
+        const uint32_t mi = a.min_ingress[o];
+        for (uint32_t i = 0; i < len; ++i) {
+          const uint32_t ki = a.ckey[(size_t)i * PAIRS + p];
+          const uint32_t si = a.cscore[(size_t)i * PAIRS + p] & 0x7F;
+          const uint64_t sti = a.stake[ki];
+          uint32_t pos = 0;
+          uint64_t cum = 0;
+          for (uint32_t j = 0; j < len; ++j) {
+            if (j == i) continue;
+            const uint32_t kj = a.ckey[(size_t)j * PAIRS + p];
+            const uint32_t sj = a.cscore[(size_t)j * PAIRS + p] & 0x7F;
+            const uint64_t stj = a.stake[kj];
+            // sort by Reverse((score, stake)); ties by ascending id (canonical order)
+            const bool before = sj > si || (sj == si && (stj > sti || (stj == sti && kj < ki)));
+            if (before) {
+              ++pos;
+              cum = cum + stj < cum ? ~0ull : cum + stj;
+            }
+          }
+          const bool pruned = pos >= mi && cum >= mis && ki != org;
+          if (pruned) {
+            a.cscore[(size_t)i * PAIRS + p] = (uint8_t)(si | PRUNED_FLAG);
+            ++npr;
+          }
+        }
+        plen = len;  // std::mem::take: the entry resets, the pruned keys stay readable
+        len = 0;
+        up = 0;
+      }
+      a.prune_round[p] = (uint8_t)(npr < 255 ? npr : 255);
+      if (npr) atomicAdd(&a.slot_prunes[o], npr);
+      meta = len | (up << 8) | (plen << 16);
+    }
+    if (APPLY && plen) {
+      // prune_connections -> PushActiveSet::prune(prunee, pruner = v, [origin])
+      // (gossip.rs:701-737, push_active_set.rs:56-71,143-151).
+      const uint32_t org = a.origin[o];
+      const uint32_t ob = a.obkt[o];
+      for (uint32_t i = 0; i < plen; ++i) {
+        const uint8_t sc = a.cscore[(size_t)i * PAIRS + p];
+        if (!(sc & PRUNED_FLAG)) continue;
+        const uint32_t u = a.ckey[(size_t)i * PAIRS + p];
+        if (u == org) continue;
+        const uint32_t b = min((uint32_t)a.bucket[u], ob);
+        const uint32_t ent = u * NB + b;
+        const uint32_t hv = a.hl[ent];
+        const uint32_t head = hv & 0xFF, L = hv >> 8;
+        const uint32_t* row = a.peers + (size_t)ent * a.ASZP;
+        for (uint32_t j = 0; j < L; ++j) {
+          uint32_t slot = head + j;
+          if (slot >= a.ASZ) slot -= a.ASZ;
+          if (row[slot] == v) {
+            atomicOr(&a.mask[(size_t)o * a.N + u], 1u << slot);
+            break;
+          }
+        }
+      }
+    }
+    a.cmeta[p] = meta;
+  }
+  if (cache_overflow) atomicOr(a.err, ERR_CACHE);
+}
+
+hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply) {
+  CpArgs a;
+  a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
+  a.min_ingress = e.min_ingress; a.thr = e.thr; a.cnt = e.cnt; a.inb = e.inb; a.cmeta = e.cmeta; a.ckey = e.ckey;
+  a.cscore = e.cscore; a.prune_round = e.prune_round; a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.err = e.err;
+  a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.ASZP = e.ASZP; a.capin = e.capin; a.PAIRS = e.PAIRS;
+  const uint32_t grid = grid_for(e.PAIRS, 256, 8192);
+  if (prune) {
+    hipError_t r = hipMemsetAsync(e.slot_prunes, 0, e.S * 4, e.st);
+    if (r != hipSuccess) return r;
+  }
+#define GS_CP(C, P, A) hipLaunchKernelGGL((k_consume_prune<C, P, A>), dim3(grid), dim3(256), 0, e.st, a)
+  if (consume && prune && apply) GS_CP(true, true, true);
+  else if (consume && !prune && !apply) GS_CP(true, false, false);
+  else if (!consume && prune && !apply) GS_CP(false, true, false);
+  else if (!consume && !prune && apply) GS_CP(false, false, true);
+  else return hipErrorInvalidValue;
+#undef GS_CP
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------ stats (R16-R22) ----
+struct StatsArgs {
+  const uint64_t* stake;
+  const uint32_t* frank;
+  const uint32_t* srank;
+  const uint32_t* by_srank;
+  const uint32_t* nfail;
+  const uint8_t* hops;
+  const uint32_t* cnt;
+  const uint8_t* egress;
+  const uint8_t* prune_round;
+  const uint32_t* slot_prunes;
+  uint32_t* egress_acc;
+  uint32_t* ingress_acc;
+  uint32_t* prune_acc;
+  uint32_t* strand;
+  uint32_t* rs_u32;
+  uint64_t* rs_ssum;
+  uint32_t* rs_hist;
+  uint64_t* hist_acc;
+  uint32_t* bm;
+  gs_round_summary* sum;
+  uint32_t N, S, W;
+};
+
+__global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
+  const uint32_t o = blockIdx.y;
+  const size_t base = (size_t)o * a.N;
+  const uint32_t nf = a.nfail[o];
+  __shared__ uint32_t h[256];
+  __shared__ uint32_t acc[3];
+  __shared__ unsigned long long ssum_s;
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) h[i] = 0;
+  if (threadIdx.x < 3) acc[threadIdx.x] = 0;
+  if (threadIdx.x == 0) ssum_s = 0;
+  __syncthreads();
+  uint32_t vis = 0, pushes = 0, sc = 0;
+  uint64_t ss = 0;
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < a.N; v += gridDim.x * blockDim.x) {
+    const size_t p = base + v;
+    const uint32_t hh = a.hops[p];
+    const uint32_t c = a.cnt[p];
+    pushes += c;
+    a.ingress_acc[p] += c;
+    a.prune_acc[p] += a.prune_round[p];
+    if (hh != 0xFF) {
+      ++vis;
+      atomicAdd(&h[hh], 1u);
+      a.egress_acc[p] += a.egress[p];
+    } else if (!(nf && a.frank[v] < nf)) {
+      a.strand[p] += 1;
+      ++sc;
+      ss += a.stake[v];
+      const uint32_t r = a.srank[v];
+      atomicOr(&a.bm[(size_t)o * a.W + (r >> 5)], 1u << (r & 31));
+    }
+  }
+  atomicAdd(&acc[0], vis);
+  atomicAdd(&acc[1], pushes);
+  atomicAdd(&acc[2], sc);
+  if (ss) atomicAdd(&ssum_s, (unsigned long long)ss);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
+    if (h[i]) atomicAdd(&a.rs_hist[o * 256 + i], h[i]);
+  if (threadIdx.x < 3 && acc[threadIdx.x]) atomicAdd(&a.rs_u32[o * 4 + threadIdx.x], acc[threadIdx.x]);
+  if (threadIdx.x == 0 && ssum_s) atomicAdd((unsigned long long*)&a.rs_ssum[o], ssum_s);
+}
+
+// k-th set bit (0-based) of a slot's stranded bitmap, found by the whole block.
+__device__ uint32_t block_kth_bit(const uint32_t* __restrict__ bm, uint32_t W, uint32_t k, uint32_t* scratch) {
+  const uint32_t T = blockDim.x, t = threadIdx.x;
+  const uint32_t chunk = (W + T - 1) / T;
+  const uint32_t lo = min(W, t * chunk), hi = min(W, lo + chunk);
+  uint32_t c = 0;
+  for (uint32_t i = lo; i < hi; ++i) c += __popc(bm[i]);
+  scratch[t] = c;
+  __syncthreads();
+  for (uint32_t off = 1; off < T; off <<= 1) {
+    const uint32_t x = t >= off ? scratch[t - off] : 0;
+    __syncthreads();
+    scratch[t] += x;
+    __syncthreads();
+  }
+  const uint32_t before = scratch[t] - c;
+  __syncthreads();
+  if (k >= before && k < before + c) {
+    uint32_t need = k - before;
+    for (uint32_t i = lo; i < hi; ++i) {
+      uint32_t w = bm[i];
+      const uint32_t pc = __popc(w);
+      if (need < pc) {
+        for (uint32_t j = 0; j < need; ++j) w &= w - 1;
+        scratch[T] = i * 32 + (__ffs(w) - 1);
+        break;
+      }
+      need -= pc;
+    }
+  }
+  __syncthreads();
+  const uint32_t r = scratch[T];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_stats_finalize(StatsArgs a, uint32_t rec_slot) {
+  const uint32_t o = blockIdx.x;
+  __shared__ uint32_t hb[256];
+  __shared__ uint32_t scratch[257];
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    hb[i] = a.rs_hist[o * 256 + i];
+    a.hist_acc[o * 256 + i] += hb[i];
+    a.rs_hist[o * 256 + i] = 0;
+  }
+  __syncthreads();
+  gs_round_summary s = {};
+  s.visited = a.rs_u32[o * 4 + 0];
+  s.pushes = a.rs_u32[o * 4 + 1];
+  s.stranded = a.rs_u32[o * 4 + 2];
+  s.prunes = a.slot_prunes[o];
+  s.stranded_stake_sum = a.rs_ssum[o];
+  // HopsStat over reached non-origin nodes (hops 1..254)
+  uint32_t count = 0;
+  uint64_t hsum = 0;
+  for (uint32_t i = 1; i < 255; ++i) { count += hb[i]; hsum += (uint64_t)i * hb[i]; }
+  s.hop_count = count;
+  s.hop_sum = hsum;
+  if (count) {
+    const uint32_t klo = count % 2 ? count / 2 : count / 2 - 1, khi = count / 2;
+    uint32_t run = 0;
+    bool got_min = false;
+    for (uint32_t i = 1; i < 255; ++i) {
+      if (!hb[i]) continue;
+      if (!got_min) { s.hop_min = i; got_min = true; }
+      s.hop_max = i;
+      if (klo >= run && klo < run + hb[i]) s.hop_med_lo = i;
+      if (khi >= run && khi < run + hb[i]) s.hop_med_hi = i;
+      run += hb[i];
+    }
+  }
+  const uint32_t* bmo = a.bm + (size_t)o * a.W;
+  const uint32_t sc = s.stranded;
+  if (sc) {
+    const uint32_t klo = sc % 2 ? sc / 2 : sc / 2 - 1, khi = sc / 2;
+    s.stranded_stake_min = a.stake[a.by_srank[block_kth_bit(bmo, a.W, 0, scratch)]];
+    s.stranded_stake_max = a.stake[a.by_srank[block_kth_bit(bmo, a.W, sc - 1, scratch)]];
+    s.stranded_med_lo = a.stake[a.by_srank[block_kth_bit(bmo, a.W, klo, scratch)]];
+    s.stranded_med_hi = a.stake[a.by_srank[block_kth_bit(bmo, a.W, khi, scratch)]];
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < a.W; i += blockDim.x) a.bm[(size_t)o * a.W + i] = 0;
+  if (threadIdx.x == 0) {
+    a.sum[(size_t)rec_slot * a.S + o] = s;
+    a.rs_u32[o * 4 + 0] = 0;
+    a.rs_u32[o * 4 + 1] = 0;
+    a.rs_u32[o * 4 + 2] = 0;
+    a.rs_ssum[o] = 0;
+  }
+}
+
+hipError_t launch_stats(Engine& e, uint32_t rec_slot) {
+  StatsArgs a;
+  a.stake = e.stake; a.frank = e.frank; a.srank = e.srank; a.by_srank = e.by_srank; a.nfail = e.nfail;
+  a.hops = e.hops; a.cnt = e.cnt; a.egress = e.egress; a.prune_round = e.prune_round; a.slot_prunes = e.slot_prunes;
+  a.egress_acc = e.egress_acc; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc; a.strand = e.strand;
+  a.rs_u32 = e.rs_u32; a.rs_ssum = e.rs_ssum; a.rs_hist = e.rs_hist; a.hist_acc = e.hist_acc; a.bm = e.bm;
+  a.sum = e.sum; a.N = e.N; a.S = e.S; a.W = e.bm_words;
+  uint32_t gx = grid_for(e.N, 256, 64);
+  hipLaunchKernelGGL(k_stats_pass, dim3(gx, e.S), dim3(256), 0, e.st, a);
+  hipLaunchKernelGGL(k_stats_finalize, dim3(e.S), dim3(256), 0, e.st, a, rec_slot);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------ readback ----
+template <class T>
+__global__ void k_gather_strided(const T* __restrict__ src, size_t stride, uint32_t n, T* __restrict__ dst) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[(size_t)i * stride];
+}
+hipError_t launch_gather_strided_u32(Engine& e, const uint32_t* src, size_t stride, uint32_t n, uint32_t* dst) {
+  hipLaunchKernelGGL(k_gather_strided<uint32_t>, dim3(grid_for(n, 256)), dim3(256), 0, e.st, src, stride, n, dst);
+  return hipGetLastError();
+}
+hipError_t launch_gather_strided_u8(Engine& e, const uint8_t* src, size_t stride, uint32_t n, uint8_t* dst) {
+  hipLaunchKernelGGL(k_gather_strided<uint8_t>, dim3(grid_for(n, 256)), dim3(256), 0, e.st, src, stride, n, dst);
+  return hipGetLastError();
+}
+
+}  // namespace gs

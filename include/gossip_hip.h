@@ -1,0 +1,188 @@
+/*
+ * gossip_hip.h -- C ABI of the MI355X push-propagation engine for gossip-sim.
+ *
+ * Drop-in boundary for the per-iteration hot path of gregcusack/gossip-sim
+ * (src/gossip_main.rs:449-514). The reference has no FFI seam of its own; every
+ * entry point below names the reference method it replaces. A Rust maintainer
+ * binds these with `extern "C"` declarations; the C++
+ * `gossip-sim` driver and the pytest/ctypes parity tests call them directly.
+ *
+ * Conventions
+ *  - Every int-returning call returns GS_OK (0) or a negative gs_status; the
+ *    message of the last failure on this thread is gs_last_error(). Nothing
+ *    throws across the ABI.
+ *  - Nodes are addressed by id = rank of the node's base58 pubkey string
+ *    (so the reference's consume tie-break, gossip.rs:639-645, is id order).
+ *    stakes[] is indexed by id.
+ *  - One engine = one HIP device + one stream + one shared active-set
+ *    trajectory, carrying n_slots independent simulations ("slots"). A slot is
+ *    one reference Cluster run: its own origin, prune/cache overlay, failed set
+ *    and statistics. Sims that share seed/fanout/active-set-size/rotation
+ *    probability (an origin-rank, min-ingress, prune-threshold or fail-nodes
+ *    sweep, or "all origins") batch into one engine.
+ *  - The engine owns all device memory. Inputs are copied at call time; outputs
+ *    go to caller buffers with explicit capacities (too small => GS_ERANGE).
+ *  - An engine is not re-entrant; use one engine per device per host thread.
+ *  - Randomness follows the Philox determinism contract: results
+ *    are a pure function of (stakes, params, slots, call sequence).
+ */
+#ifndef GOSSIP_HIP_H
+#define GOSSIP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum gs_status {
+  GS_OK = 0,
+  GS_EINVAL = -1,  /* bad argument */
+  GS_EHIP = -2,    /* HIP runtime failure (no device, launch error, ...) */
+  GS_ENOMEM = -3,  /* device or host allocation failed */
+  GS_ERANGE = -4,  /* a capacity or limit was exceeded (see gs_last_error) */
+  GS_ESTATE = -5   /* call out of order */
+} gs_status;
+
+enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24) - 1, GS_HOP_UNREACHED = 0xFF };
+enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2 };
+enum { GS_FLAG_PROFILE = 1 };
+
+typedef struct gs_params {
+  uint32_t push_fanout;         /* Config::gossip_push_fanout (gossip.rs:113) */
+  uint32_t active_set_size;     /* Config::gossip_active_set_size, 1..32 */
+  double rotation_probability;  /* Config::probability_of_rotation, [0,1] */
+  uint64_t seed;                /* Philox key of the INIT/ROTATE/DECIDE/FAIL streams */
+  int32_t device;               /* HIP device ordinal */
+  uint32_t bfs_mode;            /* GS_BFS_* (results are identical in every mode) */
+  uint32_t inbound_capacity;    /* per-(slot,node) inbound records per round; 0 = 64 */
+  uint32_t flags;               /* GS_FLAG_PROFILE: time kernels with hipEvents */
+} gs_params;
+
+typedef struct gs_slot {
+  uint32_t origin;               /* node id of the CRDS value owner (gossip_main.rs:360) */
+  uint32_t min_ingress_nodes;    /* Config::min_ingress_nodes */
+  double prune_stake_threshold;  /* Config::prune_stake_threshold */
+} gs_slot;
+
+/* Per slot, per recorded round: every integer the reference's per-round
+ * statistics are built from (gossip_main.rs:480-563). f64 summaries are
+ * computed on the host in the reference's order (gs_stats_*). */
+typedef struct gs_round_summary {
+  uint32_t visited;      /* n of RelativeMessageRedundancy: nodes reached incl. origin */
+  uint32_t pushes;       /* pushes to non-failed peers (the m increments of gossip.rs:571) */
+  uint32_t prunes;       /* prunees emitted by send_prunes (gossip.rs:684-687) */
+  uint32_t stranded;     /* unreached, non-failed nodes (gossip.rs:329-345) */
+  uint64_t hop_sum;      /* sum of hops over reached non-origin nodes */
+  uint32_t hop_count;    /* number of reached non-origin nodes */
+  uint32_t hop_min, hop_max, hop_med_lo, hop_med_hi; /* order statistics of those hops */
+  uint32_t pad0;
+  uint64_t stranded_stake_sum;
+  uint64_t stranded_stake_min, stranded_stake_max, stranded_med_lo, stranded_med_hi;
+} gs_round_summary;
+
+typedef struct gs_engine gs_engine;
+
+/* --- lifetime --------------------------------------------------------- */
+int gs_create(const gs_params* params, const uint64_t* stakes, uint32_t n_nodes, uint32_t n_slots,
+              gs_engine** out);
+void gs_destroy(gs_engine* e);
+const char* gs_last_error(void);
+int gs_set_slots(gs_engine* e, const gs_slot* slots, uint32_t n_slots);
+int gs_sync(gs_engine* e); /* waits for the stream and reports deferred device-side errors */
+
+/* --- active sets: push_active_set.rs -------------------------------------- */
+/* Node::initialize_gossip for every node (gossip.rs:805-813, gossip_main.rs:263-277). */
+int gs_init_active_sets(gs_engine* e);
+/* Overwrite / read one PushActiveSetEntry (push_active_set.rs:30) in FIFO order.
+ * Setting an entry clears the prune state of its slots for every origin. */
+int gs_set_active_set_entry(gs_engine* e, uint32_t node, uint32_t bucket, const uint32_t* peers, uint32_t len);
+int gs_get_active_set_entry(gs_engine* e, uint32_t node, uint32_t bucket, uint32_t* peers, uint32_t cap,
+                            uint32_t* len);
+
+/* --- the per-iteration steps: gossip.rs Cluster -------------------------- */
+int gs_fail_nodes(gs_engine* e, const double* fraction_per_slot); /* Cluster::fail_nodes gossip.rs:756 */
+int gs_run_gossip(gs_engine* e);                  /* Cluster::run_gossip gossip.rs:494 */
+int gs_consume_messages(gs_engine* e);            /* Cluster::consume_messages gossip.rs:618 */
+int gs_send_prunes(gs_engine* e);                 /* Cluster::send_prunes gossip.rs:657 */
+int gs_prune_connections(gs_engine* e);           /* Cluster::prune_connections gossip.rs:701 */
+int gs_chance_to_rotate(gs_engine* e, uint32_t round); /* Cluster::chance_to_rotate gossip.rs:739 */
+int gs_record_round(gs_engine* e);                /* stats inserts gossip_main.rs:480-563 */
+/* One iteration of gossip_main.rs:449-564 for every slot: run_gossip ->
+ * consume -> send_prunes -> prune_connections -> chance_to_rotate(round) ->
+ * (record != 0: the measured-round statistics). */
+int gs_round(gs_engine* e, uint32_t round, int record);
+
+/* --- readbacks (synchronise the engine stream) ----------------------------- */
+int gs_read_hops(gs_engine* e, uint32_t slot, uint8_t* hops /*[n]*/); /* distances; 0xFF = u64::MAX */
+/* orders (gossip.rs:601-607) as CSR by destination, each list in consume order
+ * (hop, then id). off has n+1 entries. */
+int gs_read_inbound(gs_engine* e, uint32_t slot, uint32_t* off, uint32_t* src, uint8_t* hop, size_t cap);
+/* prunes of the last send_prunes (pruner, prunee) pairs sorted by (pruner, prunee). */
+int gs_read_prunes(gs_engine* e, uint32_t slot, uint32_t* pruner, uint32_t* prunee, size_t cap, size_t* count);
+/* ReceivedCache entry (received_cache.rs:13-17) of `node` for the slot's origin, keys sorted. */
+int gs_read_cache(gs_engine* e, uint32_t slot, uint32_t node, uint32_t* num_upserts, uint32_t* keys,
+                  uint32_t* scores, uint32_t cap, uint32_t* len);
+/* Prune state of `node`'s entry for the slot's origin, bit i = i-th peer in FIFO order pruned. */
+int gs_read_pruned(gs_engine* e, uint32_t slot, uint32_t node, uint32_t* fifo_mask);
+/* Bulk forms for parity diffing: every entry in FIFO order (peers[(node*25+k)*active_set_size + i],
+ * len[node*25+k]); every node's cache for the slot (keys sorted, 96 per node); every node's FIFO prune mask. */
+int gs_read_active_sets(gs_engine* e, uint32_t* peers, uint8_t* len);
+int gs_read_caches(gs_engine* e, uint32_t slot, uint32_t* num_upserts, uint32_t* len, uint32_t* keys,
+                   uint32_t* scores);
+int gs_read_pruned_all(gs_engine* e, uint32_t slot, uint32_t* fifo_mask);
+/* this round's egress/ingress/prune-sent counts (gossip.rs:185-189); egress of an
+ * unreached node reads 0 */
+int gs_read_counters(gs_engine* e, uint32_t slot, uint32_t* egress, uint32_t* ingress, uint32_t* prune_sent);
+/* recorded rounds so far: out[r * n_slots + slot] */
+int gs_read_round_summaries(gs_engine* e, gs_round_summary* out, size_t cap, size_t* count);
+/* measured-round accumulators: message trackers (gossip_stats.rs:359-461), times
+ * stranded per node (gossip_stats.rs:849) and the hop histogram (raw_hop_collection) */
+int gs_read_accumulators(gs_engine* e, uint32_t slot, uint64_t* egress, uint64_t* ingress, uint64_t* prunes,
+                         uint32_t* stranded_times, uint64_t* hop_hist /*[256]*/);
+int gs_read_failed(gs_engine* e, uint32_t slot, uint8_t* failed /*[n]*/);
+/* GS_FLAG_PROFILE: summed device time of a kernel family ("bfs", "consume",
+ * "rotate", "stats") since the last reset, and its launch count. */
+int gs_kernel_time(gs_engine* e, const char* family, double* ms, uint64_t* launches);
+int gs_kernel_time_reset(gs_engine* e);
+int gs_engine_info(gs_engine* e, uint32_t* n_nodes, uint32_t* n_slots, uint32_t* bfs_mode, uint64_t* device_bytes);
+
+/* --- host-side statistics (gossip_stats.rs), f64 in the reference's order --- */
+typedef struct gs_hops_stat { double mean, median; uint64_t max, min; } gs_hops_stat;
+typedef struct gs_stat4 { double mean, median, max, min; } gs_stat4;
+/* HopsStat::new (gossip_stats.rs:47-98) over raw distances (u64::MAX = unreached). */
+int gs_hops_stat_new(const uint64_t* hops, size_t n, gs_hops_stat* out);
+/* StatCollection::calculate_stats (gossip_stats.rs:266-295). */
+int gs_stat_collection_calculate(const double* values, size_t n, gs_stat4* out);
+
+/* --- whole simulations: gossip_main.rs run_simulation ---------------------- */
+typedef struct gs_sim_config {  /* gossip.rs Config (gossip.rs:111-133) */
+  uint32_t push_fanout, active_set_size, iterations, warm_up_rounds;
+  uint32_t min_ingress_nodes, when_to_fail;
+  double rotation_probability, prune_stake_threshold, fraction_to_fail;
+  uint64_t num_buckets_stranded, num_buckets_message, num_buckets_hops;
+  int32_t test_type;  /* 0 none, 1 active-set-size, 2 min-ingress-nodes, 3 push-fanout,
+                         4 prune-stake-threshold, 5 fail-nodes, 6 origin-rank, 7 rotate-probability */
+  uint64_t seed;
+  int32_t device;
+  uint32_t bfs_mode;
+} gs_sim_config;
+
+typedef struct gs_sim_result gs_sim_result;
+/* Runs n_sims simulations that share one active-set trajectory as slots of one
+ * engine; sims differ only in origin_rank / min_ingress / threshold / fraction. */
+int gs_run_simulations(const gs_sim_config* cfg, const uint64_t* stakes, uint32_t n_nodes, uint32_t n_sims,
+                       const uint32_t* origin_ranks, const uint32_t* min_ingress, const double* thresholds,
+                       const double* fractions, gs_sim_result** out);
+void gs_result_free(gs_sim_result* r);
+/* Named arrays of a finished sim (same names as the oracle): e.g. "coverage",
+ * "rmr", "coverage_stats", "stranded", "hops_hist" ... Returns the element
+ * count (copies min(count, cap)); SIZE_MAX for an unknown name. */
+size_t gs_result_f64(const gs_sim_result* r, uint32_t sim, const char* name, double* out, size_t cap);
+size_t gs_result_u64(const gs_sim_result* r, uint32_t sim, const char* name, uint64_t* out, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOSSIP_HIP_H */

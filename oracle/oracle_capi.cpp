@@ -181,6 +181,15 @@ size_t or_sim_find_nth_largest(void* sp, size_t n) {
   const Node* nd = s->find_nth_largest(n);
   return nd ? s->index.at(nd->pk) : (size_t)-1;
 }
+// One full reference iteration (gossip_main.rs:449-473) for the CPU baseline;
+// returns the pushes to non-failed peers of this round.
+uint64_t or_sim_round(void* sp, size_t origin, double thr, size_t min_ingress, size_t asz, double p, uint32_t round) {
+  Sim* s = (Sim*)sp;
+  s->round_steps(s->nodes[origin].pk, thr, min_ingress, asz, p, round, nullptr);
+  uint64_t e = 0;
+  for (auto& kv : s->cluster.ingress_message_count) e += kv.second;
+  return e;
+}
 size_t or_sim_rank(void* sp, size_t idx) { Sim* s = (Sim*)sp; return s->rank.at(s->nodes[idx].pk); }
 size_t or_sim_visited_len(void* s) { return ((Sim*)s)->cluster.visited.size(); }
 void or_sim_distances(void* sp, uint64_t* out) {
@@ -264,6 +273,50 @@ long or_sim_entry(void* sp, size_t node, int k, uint32_t* peers, size_t cap) {
   auto& keys = s->nodes[node].active_set.e[k].keys;
   for (size_t i = 0; i < keys.size() && i < cap; ++i) peers[i] = (uint32_t)s->index.at(keys[i]);
   return (long)keys.size();
+}
+// Bulk: every entry in FIFO order, peers[(node*25+k)*cap + i] (index space), len[node*25+k].
+void or_sim_entries(void* sp, uint32_t* peers, uint8_t* len, size_t cap) {
+  Sim* s = (Sim*)sp;
+  for (size_t n = 0; n < s->nodes.size(); ++n)
+    for (int k = 0; k < NUM_PUSH_ACTIVE_SET_ENTRIES; ++k) {
+      auto& keys = s->nodes[n].active_set.e[k].keys;
+      len[n * 25 + k] = (uint8_t)keys.size();
+      for (size_t i = 0; i < cap; ++i)
+        peers[(n * 25 + k) * cap + i] = i < keys.size() ? (uint32_t)s->index.at(keys[i]) : 0xFFFFFFFFu;
+    }
+}
+// Bulk: FIFO prune mask of every node's entry for `origin` (bit i = i-th peer's filter holds origin).
+void or_sim_pruned_all(void* sp, size_t origin, uint32_t* out) {
+  Sim* s = (Sim*)sp;
+  const Pubkey& o = s->nodes[origin].pk;
+  for (size_t n = 0; n < s->nodes.size(); ++n) {
+    const uint64_t* m = opt_min(stake_of(s->stakes, s->nodes[n].pk), stake_of(s->stakes, o));
+    auto& e = s->nodes[n].active_set.e[get_stake_bucket(m)];
+    uint32_t bits = 0;
+    for (size_t i = 0; i < e.keys.size(); ++i)
+      if (e.keys[i] != o && e.filters.at(e.keys[i]).count(o)) bits |= 1u << i;
+    out[n] = bits;
+  }
+}
+// Bulk: every node's cache entry for `origin`: upserts (UINT32_MAX when absent), len, keys sorted (cap each).
+void or_sim_caches(void* sp, size_t origin, uint32_t* up, uint32_t* len, uint32_t* keys, uint32_t* scores,
+                   size_t cap) {
+  Sim* s = (Sim*)sp;
+  const Pubkey& o = s->nodes[origin].pk;
+  for (size_t n = 0; n < s->nodes.size(); ++n) {
+    auto& rc = s->nodes[n].received_cache;
+    auto it = rc.m.find(o);
+    std::vector<std::pair<uint32_t, uint64_t>> v;
+    if (it != rc.m.end())
+      for (auto& kv : it->second.nodes) v.push_back({(uint32_t)s->index.at(kv.first), kv.second});
+    std::sort(v.begin(), v.end());
+    up[n] = it == rc.m.end() ? 0xFFFFFFFFu : (uint32_t)it->second.num_upserts;
+    len[n] = (uint32_t)v.size();
+    for (size_t i = 0; i < cap; ++i) {
+      keys[n * cap + i] = i < v.size() ? v[i].first : 0xFFFFFFFFu;
+      scores[n * cap + i] = i < v.size() ? (uint32_t)v[i].second : 0;
+    }
+  }
 }
 // 1 if `origin` is in the filter of `peer` inside entry k of `node` (prune state).
 int or_sim_entry_pruned(void* sp, size_t node, int k, size_t peer, size_t origin) {

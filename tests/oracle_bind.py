@@ -95,6 +95,7 @@ def _load():
         "or_sim_fail_nodes": (C.c_long, [P, D]),
         "or_sim_find_nth_largest": (SZ, [P, SZ]),
         "or_sim_rank": (SZ, [P, SZ]),
+        "or_sim_round": (U64, [P, SZ, D, SZ, SZ, D, U32]),
         "or_sim_visited_len": (SZ, [P]),
         "or_sim_distances": (None, [P, P]),
         "or_sim_orders": (C.c_long, [P, SZ, P, P, SZ]),
@@ -110,6 +111,9 @@ def _load():
         "or_sim_stranded": (SZ, [P, P, SZ]),
         "or_sim_entry": (C.c_long, [P, SZ, I, P, SZ]),
         "or_sim_entry_pruned": (I, [P, SZ, I, SZ, SZ]),
+        "or_sim_entries": (None, [P, P, P, SZ]),
+        "or_sim_pruned_all": (None, [P, SZ, P]),
+        "or_sim_caches": (None, [P, SZ, P, P, P, P, SZ]),
         "or_sim_cache": (C.c_long, [P, SZ, SZ, P, P, P, SZ]),
         "or_sim_failed": (None, [P, P]),
         "or_sim_total_prunes": (SZ, [P]),
@@ -330,6 +334,9 @@ class Sim:
     def find_nth_largest(self, n):
         return lib.or_sim_find_nth_largest(self.h, n)
 
+    def round(self, origin, thr, min_ingress, asz, p, rnd):
+        return lib.or_sim_round(self.h, origin, thr, min_ingress, asz, p, rnd)
+
     def rank(self, i):
         return lib.or_sim_rank(self.h, i)
 
@@ -400,6 +407,25 @@ class Sim:
         out = np.zeros(64, dtype=np.uint32)
         c = lib.or_sim_entry(self.h, node, k, _ptr(out), 64)
         return [int(x) for x in out[:c]]
+
+    def entries(self, cap):
+        peers = np.zeros(self.n * 25 * cap, dtype=np.uint32)
+        lens = np.zeros(self.n * 25, dtype=np.uint8)
+        lib.or_sim_entries(self.h, _ptr(peers), _ptr(lens), cap)
+        return peers.reshape(self.n, 25, cap), lens.reshape(self.n, 25)
+
+    def pruned_all(self, origin):
+        out = np.zeros(self.n, dtype=np.uint32)
+        lib.or_sim_pruned_all(self.h, origin, _ptr(out))
+        return out
+
+    def caches(self, origin, cap=96):
+        up = np.zeros(self.n, dtype=np.uint32)
+        ln = np.zeros(self.n, dtype=np.uint32)
+        k = np.zeros(self.n * cap, dtype=np.uint32)
+        s = np.zeros(self.n * cap, dtype=np.uint32)
+        lib.or_sim_caches(self.h, origin, _ptr(up), _ptr(ln), _ptr(k), _ptr(s), cap)
+        return up, ln, k.reshape(self.n, cap), s.reshape(self.n, cap)
 
     def entry_pruned(self, node, k, peer, origin):
         return lib.or_sim_entry_pruned(self.h, node, k, peer, origin)

@@ -1,0 +1,282 @@
+"""GPU parity: the HIP engine (through the C ABI) against the oracle.
+
+Bit-exact integer comparisons throughout: hops, inbound (src, hop) lists,
+prune sets, received caches, prune state, active sets, counters, per-round
+summaries and the final f64 statistics.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import engine_bind as eb
+import oracle_bind as ob
+
+gs = eb.gs
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+U64MAX = np.uint64(2**64 - 1)
+MODES = [gs.GS_BFS_WORKGROUP, gs.GS_BFS_LEVEL]
+
+
+# ------------------------------------------------------------ reference KATs ----
+def six_node():
+    d = json.load(open(os.path.join(HERE, "golden", "six_node_cluster.json")))
+    pks = [bytes.fromhex(h) for h in d["pubkeys_hex"]]
+    ids = gs.ids_from_pubkeys(pks)  # pubkey-order index -> node id (base58 rank)
+    stakes_by_id = np.zeros(6, dtype=np.uint64)
+    for i, s in enumerate(d["stakes"]):
+        stakes_by_id[ids[i]] = s
+    return d, ids, stakes_by_id
+
+
+def upload_entries(eng, d, ids):
+    for n, ks in d["entries"].items():
+        for k, peers in ks.items():
+            if peers:
+                eng.set_entry(ids[int(n)], int(k), [ids[p] for p in peers])
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_mst_kat_on_gpu(mode):
+    """gossip.rs test_mst (1040-1163) through the HIP BFS."""
+    d, ids, st = six_node()
+    eng = gs.Engine(st, 1, fanout=2, active_set_size=12, rotation_probability=0.2, seed=1, bfs_mode=mode)
+    upload_entries(eng, d, ids)
+    eng.set_slots([ids[5]])
+    eng.run_gossip()
+    dist = eng.distances(0)
+    assert [int(dist[ids[i]]) for i in range(6)] == d["expect_distances"]
+    lists = eng.inbound_lists(0)
+    inv = {v: k for k, v in enumerate(ids)}
+    assert [len(lists[ids[i]]) for i in range(5)] == d["expect_num_inbound"]
+    assert lists[ids[5]] == []  # the origin never receives (orders has no key for it)
+    for dest, src, hop in d["expect_hops"]:
+        got = {inv[s]: h for s, h in lists[ids[dest]]}
+        assert got[src] == hop
+    e, i, p = eng.counters(0)
+    assert int(i.sum()) == int(e.sum()) == sum(d["expect_num_inbound"])
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_pruning_kat_on_gpu(mode):
+    """gossip_main.rs test_pruning (1071-1163): no prunes before iteration 19, then {3->M, M->h, j->P}."""
+    d, ids, st = six_node()
+    eng = gs.Engine(st, 1, fanout=2, active_set_size=12, rotation_probability=0.2, seed=1, bfs_mode=mode)
+    upload_entries(eng, d, ids)
+    eng.set_slots([ids[5]], min_ingress=2, thresholds=0.15)
+    inv = {v: k for k, v in enumerate(ids)}
+    for it in range(21):
+        eng.run_gossip()
+        assert (eng.hops(0) != 0xFF).sum() == 6
+        eng.consume_messages()
+        eng.send_prunes()
+        prunes = sorted((inv[a], inv[b]) for a, b in eng.prunes(0))
+        if it <= 18:
+            assert prunes == []
+        if it == 19:
+            assert prunes == sorted(tuple(x) for x in d["expect_prunes_iteration_19"])
+        eng.prune_connections()
+        eng.chance_to_rotate(it)
+
+
+# ------------------------------------------------------ Philox-mode parity ----
+def make_pair(n, origin_ranks, *, asz=12, fanout=6, p=0.013333, seed=7, thr=0.15, mi=2, mode=gs.GS_BFS_AUTO):
+    pks, st = eb.synth.network(n)
+    S = len(origin_ranks)
+    eng = gs.Engine(st, S, fanout=fanout, active_set_size=asz, rotation_probability=p, seed=seed, bfs_mode=mode)
+    sims = [ob.Sim(ob.PHILOX, seed, pks, st, fanout) for _ in range(S)]
+    origins = [sims[0].find_nth_largest(r) for r in origin_ranks]
+    eng.set_slots(origins, mi, thr)
+    eng.init_active_sets()
+    for s in sims:
+        s.init_philox(asz)
+    return eng, sims, origins, st
+
+
+def assert_entries(eng, sim, asz):
+    gp, gl = eng.active_sets()
+    op, ol = sim.entries(asz)
+    np.testing.assert_array_equal(gl, ol)
+    np.testing.assert_array_equal(np.where(gp == 0xFFFFFFFF, 0, gp), np.where(op == 0xFFFFFFFF, 0, op))
+
+
+@pytest.mark.parametrize("n,asz", [(300, 12), (200, 5), (64, 32), (9, 12), (14, 12)])
+def test_init_active_sets_parity(n, asz):
+    """gs_init_active_sets == PushActiveSet::rotate from empty entries (incl. N-1 <= size)."""
+    eng, sims, _, _ = make_pair(n, [1], asz=asz)
+    assert_entries(eng, sims[0], asz)
+
+
+def run_parity(n, ranks, rounds, *, p, mode, thr=0.15, mi=2, asz=12, fanout=6, fail_at=None, fractions=None,
+               full_every=5):
+    eng, sims, origins, st = make_pair(n, ranks, asz=asz, fanout=fanout, p=p, thr=thr, mi=mi, mode=mode)
+    thr_v = np.broadcast_to(np.asarray(thr, dtype=float), (len(ranks),))
+    mi_v = np.broadcast_to(np.asarray(mi), (len(ranks),))
+    total_prunes = 0
+    for r in range(rounds):
+        if fail_at is not None and r == fail_at:
+            eng.fail_nodes(fractions)
+            for s, f in zip(sims, fractions):
+                s.fail_nodes(f)
+            for k, s in enumerate(sims):
+                np.testing.assert_array_equal(eng.failed(k), s.failed())
+        eng.run_gossip()
+        for k, (s, o) in enumerate(zip(sims, origins)):
+            s.run_gossip(o)
+            np.testing.assert_array_equal(eng.distances(k), s.distances(), err_msg=f"hops slot {k} round {r}")
+            lists = eng.inbound_lists(k)
+            for v in range(n):
+                want = s.orders(v)
+                assert lists[v] == ([] if want is None else want), f"inbound slot {k} node {v} round {r}"
+        eng.consume_messages()
+        eng.send_prunes()
+        for k, (s, o) in enumerate(zip(sims, origins)):
+            s.consume_messages(o)
+            s.send_prunes(o, float(thr_v[k]), int(mi_v[k]))
+            assert eng.prunes(k) == s.prunes(), f"prunes slot {k} round {r}"
+            total_prunes += len(s.prunes())
+            if r % full_every == 0 or r == rounds - 1:
+                up, ln, keys, sc = eng.caches(k)
+                oup, oln, okeys, osc = s.caches(o)
+                has = oup != 0xFFFFFFFF
+                np.testing.assert_array_equal(up[has], oup[has])
+                np.testing.assert_array_equal(up[~has], 0)
+                np.testing.assert_array_equal(ln, oln)
+                np.testing.assert_array_equal(keys, okeys)
+                np.testing.assert_array_equal(sc, osc)
+        eng.prune_connections()
+        for k, (s, o) in enumerate(zip(sims, origins)):
+            s.prune_connections()
+            e, i, pr = eng.counters(k)
+            oe, oi, op = s.counters()
+            np.testing.assert_array_equal(e, np.where(oe == U64MAX, 0, oe))
+            np.testing.assert_array_equal(i, np.where(oi == U64MAX, 0, oi))
+            np.testing.assert_array_equal(pr, op)
+            np.testing.assert_array_equal(eng.pruned_all(k), s.pruned_all(o), err_msg=f"prune state round {r}")
+        eng.chance_to_rotate(r)
+        for s in sims:
+            s.chance_to_rotate(asz, p, r)
+        if r % full_every == 0 or r == rounds - 1:
+            assert_entries(eng, sims[0], asz)
+            for k, (s, o) in enumerate(zip(sims, origins)):
+                np.testing.assert_array_equal(eng.pruned_all(k), s.pruned_all(o))
+    return total_prunes
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_round_by_round_parity(mode):
+    """Every step of 45 rounds, 5 origins, heavy rotation: state identical to the oracle."""
+    total = run_parity(240, [1, 2, 7, 60, 240], 45, p=0.08, mode=mode, full_every=4)
+    assert total > 0  # the ~20-round prune waves were exercised
+
+
+def test_parity_sweep_params_and_failures():
+    """Per-slot thresholds / min-ingress and fail-nodes (failed peers burn fanout slots)."""
+    run_parity(180, [1, 3, 5, 9], 42, p=0.03, mode=gs.GS_BFS_LEVEL, thr=[0.0, 0.15, 0.4, 1.0], mi=[0, 2, 3, 1],
+               fail_at=2, fractions=[0.1, 0.2, 0.3, 0.5], full_every=6)
+
+
+def test_parity_small_fanout_and_asz():
+    run_parity(150, [1, 4], 30, p=0.05, mode=gs.GS_BFS_WORKGROUP, asz=7, fanout=3, full_every=5)
+
+
+def test_fused_round_matches_steps():
+    """gs_round (fused consume+prune+apply) == the step-by-step calls."""
+    pks, st = eb.synth.network(260)
+    a = gs.Engine(st, 4, seed=3, rotation_probability=0.05)
+    b = gs.Engine(st, 4, seed=3, rotation_probability=0.05)
+    for e in (a, b):
+        e.set_slots([0, 10, 100, 200])
+        e.init_active_sets()
+    for r in range(30):
+        a.round(r, record=r >= 10)
+        b.run_gossip(); b.consume_messages(); b.send_prunes(); b.prune_connections(); b.chance_to_rotate(r)
+        if r >= 10:
+            b.record_round()
+    for k in range(4):
+        np.testing.assert_array_equal(a.hops(k), b.hops(k))
+        np.testing.assert_array_equal(a.pruned_all(k), b.pruned_all(k))
+        for x, y in zip(a.caches(k), b.caches(k)):
+            np.testing.assert_array_equal(x, y)
+        for x, y in zip(a.accumulators(k), b.accumulators(k)):
+            np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(a.summaries(), b.summaries())
+
+
+# --------------------------------------------------------- whole simulation ----
+F64_NAMES = ["coverage", "rmr", "branching", "hop_mean", "hop_median", "coverage_stats", "rmr_stats",
+             "branching_stats", "aggregate_hops", "ldh", "stranded", "stranded_round_mean", "stranded_round_median"]
+U64_NAMES = ["origin", "hop_max", "hop_min", "aggregate_hops", "ldh", "stranded", "stranded_times",
+             "stranded_round_count", "stranded_round_max", "stranded_round_min", "hops_hist", "stranded_hist",
+             "egress_hist", "ingress_hist", "prune_hist", "egress_cpb", "validator_hist", "hist_errors",
+             "failed_count"]
+
+
+def compare_sim(n, *, ranks, iterations, warm, test_type=0, fractions=None, thresholds=None, min_ingress=None, **kw):
+    pks, st = eb.synth.network(n)
+    res = gs.run_simulations(st, n_sims=len(ranks), origin_ranks=ranks, iterations=iterations, warm_up=warm,
+                             test_type=test_type, fractions=fractions, thresholds=thresholds,
+                             min_ingress=min_ingress, **kw)
+    for k, rank in enumerate(ranks):
+        okw = dict(kw)
+        if fractions is not None:
+            okw["fraction_to_fail"] = fractions[k]
+        if thresholds is not None:
+            okw["thr"] = thresholds[k]
+        if min_ingress is not None:
+            okw["min_ingress"] = min_ingress[k]
+        okw.pop("bfs_mode", None)
+        o = ob.run_simulation(pks, st, origin_rank=rank, iterations=iterations, warm_up=warm, test_type=test_type,
+                              **okw)
+        for name in F64_NAMES:
+            np.testing.assert_array_equal(res.f64(k, name), o.f64(name), err_msg=f"sim {k} {name}")
+        for name in U64_NAMES:
+            np.testing.assert_array_equal(res.u64(k, name), o.u64(name), err_msg=f"sim {k} {name}")
+
+
+def test_simulation_stats_parity_origin_rank_sweep():
+    compare_sim(300, ranks=[1, 2, 3], iterations=70, warm=20, seed=11, p=0.02)
+
+
+def test_simulation_stats_parity_fail_nodes():
+    compare_sim(250, ranks=[1, 1, 1], iterations=50, warm=10, test_type=5, fractions=[0.1, 0.25, 0.4],
+                when_to_fail=5, seed=5, bfs_mode=gs.GS_BFS_LEVEL)
+
+
+def test_simulation_stats_parity_threshold_sweep():
+    compare_sim(220, ranks=[1, 1, 1], iterations=45, warm=5, thresholds=[0.05, 0.2, 0.6], min_ingress=[2, 1, 4],
+                seed=9)
+
+
+# ---------------------------------------------------- size-independent checks ----
+def test_large_network_invariants():
+    """N = 200k, level-synchronous BFS: properties that hold at any size."""
+    n = 200_000
+    st = eb.synth.power_law_stakes(n)  # id order is irrelevant to these invariants
+    eng = gs.Engine(st, 2, seed=21, bfs_mode=gs.GS_BFS_LEVEL)
+    eng.set_slots([0, n // 2])
+    eng.init_active_sets()
+    for r in range(3):
+        eng.round(r, record=True)
+    peers, lens = eng.active_sets()
+    assert (lens == 12).all()
+    srt = np.sort(peers, axis=2)
+    assert (np.diff(srt.astype(np.int64), axis=2) != 0).all()  # no duplicate peers in an entry
+    assert (peers != np.arange(n, dtype=np.uint32)[:, None, None]).all()  # never yourself
+    summ = eng.summaries()
+    for k in range(2):
+        hops = eng.hops(k)
+        off, src, hop = eng.inbound(k, cap=8 * n)
+        e, i, _ = eng.counters(k)
+        assert int(i.sum()) == int(e.sum()) == int(off[-1]) == int(summ[-1, k]["pushes"])
+        assert int((hops != 0xFF).sum()) == int(summ[-1, k]["visited"])
+        # BFS: every reached non-origin node has an inbound record from hop-1, each record's hop is src hop + 1
+        h = hops.astype(np.int64)
+        dest = np.repeat(np.arange(n), np.diff(off).astype(np.int64))
+        assert (hop.astype(np.int64)[:off[-1]] == h[src[:off[-1]]] + 1).all()
+        first = hop[off[:-1][np.diff(off) > 0]]
+        reached = np.diff(off) > 0
+        assert (first.astype(np.int64) == h[reached]).all()
+        assert (dest >= 0).all()
