@@ -17,6 +17,19 @@ constexpr uint32_t CACHE_LIMIT = 50; // ReceivedCacheEntry::CAPACITY
 constexpr uint32_t MIN_NUM_UPSERTS = 20;
 constexpr uint32_t PRUNED_FLAG = 0x80u;
 
+// Debug builds (make DEBUG_BOUNDS=1): every guarded index is checked; a violation
+// prints, raises ERR_BOUNDS and the access is skipped instead of faulting.
+constexpr uint32_t ERR_BOUNDS = 0x100u;
+#ifdef GS_DEBUG_BOUNDS
+#define GS_OOB(idx, size, err, tag)                                                                     \
+  ((size_t)(idx) >= (size_t)(size)                                                                      \
+       ? (printf("GS_OOB %s: %llu >= %llu\n", tag, (unsigned long long)(idx), (unsigned long long)(size)), \
+          atomicOr((err), ERR_BOUNDS), true)                                                            \
+       : false)
+#else
+#define GS_OOB(idx, size, err, tag) false
+#endif
+
 __host__ __device__ inline uint64_t weight(int k, int bucket) {
   // (min(bucket, k) + 1)^2 (push_active_set.rs:97-111)
   uint64_t b = (uint64_t)(bucket < k ? bucket : k) + 1;

@@ -110,6 +110,7 @@ static int check_err(Engine* e) {
                                " pushes in one round; recreate the engine with a larger inbound_capacity");
   if (f & ERR_CACHE) return fail(GS_ERANGE, "received-cache capacity (96 keys) exceeded");
   if (f & ERR_DEPTH) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
+  if (f & ERR_BOUNDS) return fail(GS_ERANGE, "debug bounds check failed (see GS_OOB lines on stdout)");
   return GS_OK;
 }
 
@@ -197,6 +198,8 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   ALLOC(e->rot_list, N, 0);
   ALLOC(e->rot_count, 1, 0);
   ALLOC(e->rot_changed, N * NB, 0);
+  ALLOC(e->work, PAIRS, 0);
+  ALLOC(e->work_count, 1, 0);
   ALLOC(e->rs_u32, S * 4, 0);
   ALLOC(e->rs_ssum, S, 0);
   ALLOC(e->rs_hist, S * 256, 0);
@@ -367,10 +370,10 @@ static int need_slots(Engine* e) {
   return GS_OK;
 }
 
-static int do_bfs(Engine* e) {
+static int do_bfs(Engine* e, bool record) {
   hipEvent_t t0;
   e->tbegin("bfs", &t0);
-  hipError_t r = launch_bfs(*e);
+  hipError_t r = launch_bfs(*e, record);
   e->tend("bfs", t0);
   if (r == hipErrorNotSupported) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
   HIPC(r);
@@ -380,13 +383,13 @@ static int do_bfs(Engine* e) {
 int gs_run_gossip(gs_engine* eh) {
   ENGINE(eh);
   if (int s = need_slots(e)) return s;
-  return do_bfs(e);
+  return do_bfs(e, false);
 }
 
-static int do_cp(Engine* e, bool c, bool p, bool a) {
+static int do_cp(Engine* e, bool c, bool p, bool a, bool record = false) {
   hipEvent_t t0;
   e->tbegin("consume", &t0);
-  hipError_t r = launch_consume_prune(*e, c, p, a);
+  hipError_t r = launch_consume_prune(*e, c, p, a, record);
   e->tend("consume", t0);
   HIPC(r);
   return GS_OK;
@@ -418,25 +421,30 @@ static int drain_summaries(Engine* e) {
   return GS_OK;
 }
 
-int gs_record_round(gs_engine* eh) {
-  ENGINE(eh);
-  if (int s = need_slots(e)) return s;
+static int do_stats(Engine* e, int mode) {
   hipEvent_t t0;
   e->tbegin("stats", &t0);
-  hipError_t r = launch_stats(*e, e->sum_used);
+  hipError_t r = launch_stats(*e, e->sum_used, mode);
   e->tend("stats", t0);
   HIPC(r);
   if (++e->sum_used == e->sum_cap) return drain_summaries(e);
   return GS_OK;
 }
 
+int gs_record_round(gs_engine* eh) {
+  ENGINE(eh);
+  if (int s = need_slots(e)) return s;
+  return do_stats(e, 0);
+}
+
 int gs_round(gs_engine* eh, uint32_t round, int record) {
   ENGINE(eh);
   if (int s = need_slots(e)) return s;
-  if (int s = do_bfs(e)) return s;
-  if (int s = do_cp(e, true, true, true)) return s;
+  const bool rec = record != 0;
+  if (int s = do_bfs(e, rec)) return s;
+  if (int s = do_cp(e, true, true, true, rec)) return s;
   if (int s = gs_chance_to_rotate(eh, round)) return s;
-  if (record) return gs_record_round(eh);
+  if (rec) return do_stats(e, e->bfs_mode == GS_BFS_WORKGROUP ? 2 : 1);
   return GS_OK;
 }
 

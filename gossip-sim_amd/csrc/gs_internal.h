@@ -67,6 +67,9 @@ struct Engine {
   uint32_t* rot_list = nullptr;
   uint32_t* rot_count = nullptr;
   uint32_t* rot_changed = nullptr;
+  // fused consume -> prune worklist
+  uint32_t* work = nullptr;
+  uint32_t* work_count = nullptr;
   // stats
   uint32_t* rs_u32 = nullptr;   // per slot: visited, pushes, stranded, pad
   uint64_t* rs_ssum = nullptr;  // per slot: stranded stake sum
@@ -96,10 +99,10 @@ hipError_t launch_init_entries(Engine& e);
 hipError_t launch_fail_keys(Engine& e, uint64_t* keys, uint32_t* ids);
 hipError_t launch_scatter_rank(Engine& e, const uint32_t* sorted_ids, uint32_t* rank_out);
 hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket, uint32_t bits);
-hipError_t launch_bfs(Engine& e);
-hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply);
+hipError_t launch_bfs(Engine& e, bool record);
+hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
 hipError_t launch_rotate(Engine& e, uint32_t round);
-hipError_t launch_stats(Engine& e, uint32_t rec_index);
+hipError_t launch_stats(Engine& e, uint32_t rec_index, int mode);
 hipError_t launch_gather_strided_u32(Engine& e, const uint32_t* src, size_t stride, uint32_t n, uint32_t* dst);
 hipError_t launch_gather_strided_u8(Engine& e, const uint8_t* src, size_t stride, uint32_t n, uint8_t* dst);
 

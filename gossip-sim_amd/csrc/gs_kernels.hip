@@ -261,6 +261,17 @@ struct BfsArgs {
   uint8_t* egress;
   uint32_t* lvl;
   uint32_t* err;
+  // measured-round accumulation (record != 0)
+  uint32_t* egress_acc;
+  const uint64_t* stake;
+  const uint32_t* srank;
+  uint32_t* strand;
+  uint32_t* bm;
+  uint32_t* rs_u32;
+  uint64_t* rs_ssum;
+  uint32_t* rs_hist;
+  uint32_t W;
+  int record;
   uint32_t N, S, ASZ, fanout, capin;
   size_t PAIRS;
 };
@@ -305,17 +316,101 @@ __device__ inline uint32_t taken_slots(const uint32_t (&row)[ASZP], uint32_t hea
 
 __device__ inline uint32_t lane_id() { return __lane_id(); }
 
-// Workgroup-per-slot BFS: hop table, in-degree counters and both frontier
-// queues live in LDS (9 bytes per node), so the whole level loop runs with
+// Inclusive prefix sum over the 64 lanes of a wave (all lanes must be active).
+__device__ inline uint32_t wave_incl_scan(uint32_t x) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, off);
+    if (lane >= (uint32_t)off) x += y;
+  }
+  return x;
+}
+
+// Expands one frontier node u of slot o at level d (Cluster::run_gossip body,
+// gossip.rs:511-609), in three phases so that no memory round trip waits on
+// another: (1) every in-degree atomic of the node's pushes is issued back to
+// back; (2) their results are used: the (hop, src) record, first-visit hop;
+// (3) the newly visited peers are appended to the next frontier with ONE
+// wave-aggregated reservation. `valid` lanes expand; the rest only join the
+// wave collectives. CNT/HOPS index by peer (LDS tables, or global + base).
+template <int ASZP, class QT, bool LDS_TAIL>
+__device__ inline uint32_t expand_node(const BfsArgs& a, bool valid, uint32_t u, uint32_t ob, uint32_t org,
+                                       uint32_t nf, uint32_t pmask, size_t base, uint32_t d, uint32_t* cntp,
+                                       uint8_t* hopsp, QT* nxt, uint32_t* tail, size_t qoff, bool& overflow) {
+  uint32_t row[ASZP];
+  uint32_t pushm = 0;
+  if (valid && GS_OOB(u, a.N, a.err, "expand u")) valid = false;
+  if (valid) {
+    const uint32_t b = min((uint32_t)a.bucket[u], ob);
+    const uint32_t ent = u * NB + b;
+    const uint32_t hv = a.hl[ent];
+    load_row<ASZP>(a.peers + (size_t)ent * ASZP, row);
+    pushm = taken_slots<ASZP>(row, hv & 0xFF, hv >> 8, a.ASZ, pmask, org, a.fanout);
+#ifdef GS_DEBUG_BOUNDS
+    for (int s = 0; s < ASZP; ++s)
+      if (((pushm >> s) & 1u) && GS_OOB(row[s], a.N, a.err, "expand peer")) pushm &= ~(1u << s);
+#endif
+    if (nf) {  // failed peers burn their fanout slot (gossip.rs:538-541)
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s)
+        if (((pushm >> s) & 1u) && a.frank[row[s]] < nf) pushm &= ~(1u << s);
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) row[s] = 0;
+  }
+  uint32_t old[ASZP];
+#pragma unroll
+  for (int s = 0; s < ASZP; ++s) old[s] = ((pushm >> s) & 1u) ? atomicAdd(&cntp[row[s]], 1u) : 1u;
+  asm volatile("" ::: "memory");
+  const uint32_t rec = ((d + 1) << 24) | u;
+  uint32_t newm = 0;
+#pragma unroll
+  for (int s = 0; s < ASZP; ++s) {
+    if (!((pushm >> s) & 1u)) continue;
+    if (old[s] < a.capin) a.inb[(size_t)old[s] * a.PAIRS + base + row[s]] = rec;
+    else overflow = true;
+    if (old[s] == 0) {
+      newm |= 1u << s;
+      hopsp[row[s]] = (uint8_t)(d + 1);
+    }
+  }
+  const uint32_t k = __popc(newm);
+  uint32_t idx;
+  if (LDS_TAIL) {  // LDS counter: one per-lane atomic is a single round trip
+    idx = k ? atomicAdd(tail, k) : 0;
+  } else {         // global counter: one atomic per wave after a wave prefix sum
+    const uint32_t incl = wave_incl_scan(k);
+    const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+    uint32_t qb = 0;
+    if (lane_id() == 0 && total) qb = atomicAdd(tail, total);
+    idx = (uint32_t)__shfl((int)qb, 0) + incl - k;
+  }
+#pragma unroll
+  for (int s = 0; s < ASZP; ++s)
+    if ((newm >> s) & 1u) {
+      if (GS_OOB(idx, LDS_TAIL ? a.N : a.PAIRS, a.err, "queue idx")) continue;
+      nxt[idx++] = (QT)(qoff + row[s]);
+    }
+  return __popc(pushm);
+}
+
+// Workgroup-per-slot BFS: hop table, in-degree counters, egress and both
+// frontier queues live in LDS (10 bytes per node), so the level loop needs
 // workgroup barriers only. First visit = the in-degree atomic returning 0.
 template <int ASZP>
 __global__ __launch_bounds__(256) void k_bfs_wg(BfsArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t N = a.N;
-  uint32_t* ctrl = reinterpret_cast<uint32_t*>(smem);  // [0] frontier size, [1] next size, [2] err
-  uint32_t* cnt_l = ctrl + 4;
+  // [0] frontier size, [1] next size, [2] err, [4..6] visited/pushes/stranded, [8..9] stranded stake (u64)
+  uint32_t* ctrl = reinterpret_cast<uint32_t*>(smem);
+  unsigned long long* ssum_l = reinterpret_cast<unsigned long long*>(ctrl + 8);
+  uint32_t* hist_l = ctrl + 16;
+  uint32_t* cnt_l = hist_l + 256;
   uint8_t* hops_l = reinterpret_cast<uint8_t*>(cnt_l + N);
-  uint16_t* q0 = reinterpret_cast<uint16_t*>(hops_l + ((N + 3) & ~3u));
+  uint8_t* eg_l = hops_l + ((N + 3) & ~3u);
+  uint16_t* q0 = reinterpret_cast<uint16_t*>(eg_l + ((N + 3) & ~3u));
   uint16_t* q1 = q0 + ((N + 1) & ~1u);
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   for (uint32_t o = blockIdx.x; o < a.S; o += gridDim.x) {
@@ -323,59 +418,73 @@ __global__ __launch_bounds__(256) void k_bfs_wg(BfsArgs a) {
     const uint32_t ob = a.obkt[o];
     const uint32_t nf = a.nfail[o];
     const size_t base = (size_t)o * N;
-    for (uint32_t v = tid; v < N; v += bd) { cnt_l[v] = 0; hops_l[v] = 0xFF; }
+    for (uint32_t v = tid; v < N; v += bd) { cnt_l[v] = 0; hops_l[v] = 0xFF; eg_l[v] = 0; }
+    for (uint32_t i = tid; i < 256; i += bd) hist_l[i] = 0;
     __syncthreads();
-    if (tid == 0) { ctrl[0] = 1; ctrl[1] = 0; ctrl[2] = 0; hops_l[org] = 0; q0[0] = (uint16_t)org; }
+    if (tid == 0) {
+      ctrl[0] = 1; ctrl[1] = 0; ctrl[2] = 0; ctrl[4] = 0; ctrl[5] = 0; ctrl[6] = 0; *ssum_l = 0;
+      hops_l[org] = 0; q0[0] = (uint16_t)org;
+    }
     __syncthreads();
     uint16_t* cur = q0;
     uint16_t* nxt = q1;
+    bool overflow = false;
     for (uint32_t d = 0;; ++d) {
       const uint32_t qn = ctrl[0];
       if (qn == 0) break;
       if (d + 1 >= 255) { if (tid == 0) atomicOr(a.err, ERR_DEPTH); break; }
-      const uint32_t rec_hop = (d + 1) << 24;
-      for (uint32_t i = tid; i < qn; i += bd) {
-        const uint32_t u = cur[i];
-        const uint32_t b = min((uint32_t)a.bucket[u], ob);
-        const uint32_t ent = u * NB + b;
-        const uint32_t hv = a.hl[ent];
-        uint32_t row[ASZP];
-        load_row<ASZP>(a.peers + (size_t)ent * ASZP, row);
-        const uint32_t phys = taken_slots<ASZP>(row, hv & 0xFF, hv >> 8, a.ASZ, a.mask[base + u], org, a.fanout);
-        uint32_t pushes = 0;
-#pragma unroll
-        for (int s = 0; s < ASZP; ++s) {
-          const uint32_t peer = row[s];
-          bool push = (phys >> s) & 1u;
-          if (push && nf) push = a.frank[peer] >= nf;  // failed peers burn the fanout slot (gossip.rs:538-541)
-          bool is_new = false;
-          if (push) {
-            const uint32_t old = atomicAdd(&cnt_l[peer], 1u);
-            if (old < a.capin) a.inb[(size_t)old * a.PAIRS + base + peer] = rec_hop | u;
-            else ctrl[2] = 1;
-            is_new = old == 0;
-            if (is_new) hops_l[peer] = (uint8_t)(d + 1);
-            ++pushes;
-          }
-          const unsigned long long bal = __ballot(is_new);
-          if (bal) {
-            const int leader = __ffsll((long long)bal) - 1;
-            uint32_t qb = 0;
-            if ((int)lane_id() == leader) qb = atomicAdd(&ctrl[1], (uint32_t)__popcll(bal));
-            qb = __shfl(qb, leader);
-            if (is_new) nxt[qb + __popcll(bal & ((1ull << lane_id()) - 1))] = (uint16_t)peer;
-          }
-        }
-        a.egress[base + u] = (uint8_t)pushes;
+      for (uint32_t i0 = 0; i0 < qn; i0 += bd) {  // uniform trip count: whole waves stay active
+        const bool valid = i0 + tid < qn;
+        const uint32_t u = valid ? cur[i0 + tid] : 0;
+        const uint32_t pm = valid ? a.mask[base + u] : 0;
+        const uint32_t pushes =
+            expand_node<ASZP, uint16_t, true>(a, valid, u, ob, org, nf, pm, base, d, cnt_l, hops_l, nxt, &ctrl[1], 0,
+                                        overflow);
+        if (valid) eg_l[u] = (uint8_t)pushes;
       }
       __syncthreads();
       if (tid == 0) { ctrl[0] = ctrl[1]; ctrl[1] = 0; }
       uint16_t* t = cur; cur = nxt; nxt = t;
       __syncthreads();
     }
+    if (overflow) ctrl[2] = 1;
+    uint32_t vis = 0, pushes = 0, sc = 0;
+    uint64_t ss = 0;
     for (uint32_t v = tid; v < N; v += bd) {
-      a.hops[base + v] = hops_l[v];
-      a.cnt[base + v] = cnt_l[v];
+      const uint32_t h = hops_l[v], c = cnt_l[v], eg = eg_l[v];
+      a.hops[base + v] = (uint8_t)h;
+      a.cnt[base + v] = c;
+      a.egress[base + v] = (uint8_t)eg;
+      if (a.record) {  // the measured-round statistics, fused (gossip_main.rs:480-514)
+        pushes += c;
+        if (eg) a.egress_acc[base + v] += eg;
+        if (h != 0xFF) {
+          ++vis;
+          atomicAdd(&hist_l[h], 1u);
+        } else if (!(nf && a.frank[v] < nf)) {
+          a.strand[base + v] += 1;
+          ++sc;
+          ss += a.stake[v];
+          const uint32_t r = a.srank[v];
+          atomicOr(&a.bm[(size_t)o * a.W + (r >> 5)], 1u << (r & 31));
+        }
+      }
+    }
+    if (a.record) {
+      atomicAdd(&ctrl[4], vis);
+      atomicAdd(&ctrl[5], pushes);
+      atomicAdd(&ctrl[6], sc);
+      if (ss) atomicAdd(ssum_l, (unsigned long long)ss);
+    }
+    __syncthreads();
+    if (a.record) {
+      for (uint32_t i = tid; i < 256; i += bd) a.rs_hist[o * 256 + i] = hist_l[i];
+      if (tid == 0) {
+        a.rs_u32[o * 4 + 0] = ctrl[4];
+        a.rs_u32[o * 4 + 1] = ctrl[5];
+        a.rs_u32[o * 4 + 2] = ctrl[6];
+        a.rs_ssum[o] = *ssum_l;
+      }
     }
     if (tid == 0 && ctrl[2]) atomicOr(a.err, ERR_INBOUND);
     __syncthreads();
@@ -397,46 +506,25 @@ __global__ __launch_bounds__(256) void k_bfs_level(BfsArgs a, uint32_t d, const 
                                                   uint32_t* __restrict__ qnxt) {
   const uint32_t qn = a.lvl[d];
   const uint32_t N = a.N;
-  const uint32_t rec_hop = (d + 1) << 24;
   bool overflow = false;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < qn; i += gridDim.x * blockDim.x) {
-    const uint32_t p = qcur[i];
+  for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < qn; i0 += gridDim.x * blockDim.x) {
+    const uint32_t i = i0 + threadIdx.x;
+    const bool valid = i < qn;
+    uint32_t p = valid ? qcur[i] : 0;
+    if (valid && GS_OOB(p, a.PAIRS, a.err, "level frontier pair")) p = 0;
     const uint32_t o = p / N;
     const uint32_t u = p - o * N;
     const size_t base = (size_t)o * N;
     const uint32_t org = a.origin[o];
     const uint32_t nf = a.nfail[o];
-    const uint32_t b = min((uint32_t)a.bucket[u], (uint32_t)a.obkt[o]);
-    const uint32_t ent = u * NB + b;
-    const uint32_t hv = a.hl[ent];
-    uint32_t row[ASZP];
-    load_row<ASZP>(a.peers + (size_t)ent * ASZP, row);
-    const uint32_t phys = taken_slots<ASZP>(row, hv & 0xFF, hv >> 8, a.ASZ, a.mask[p], org, a.fanout);
-    uint32_t pushes = 0;
-#pragma unroll
-    for (int s = 0; s < ASZP; ++s) {
-      const uint32_t peer = row[s];
-      bool push = (phys >> s) & 1u;
-      if (push && nf) push = a.frank[peer] >= nf;
-      bool is_new = false;
-      if (push) {
-        const uint32_t old = atomicAdd(&a.cnt[base + peer], 1u);
-        if (old < a.capin) a.inb[(size_t)old * a.PAIRS + base + peer] = rec_hop | u;
-        else overflow = true;
-        is_new = old == 0;
-        if (is_new) a.hops[base + peer] = (uint8_t)(d + 1);
-        ++pushes;
-      }
-      const unsigned long long bal = __ballot(is_new);
-      if (bal) {
-        const int leader = __ffsll((long long)bal) - 1;
-        uint32_t qb = 0;
-        if ((int)lane_id() == leader) qb = atomicAdd(&a.lvl[d + 1], (uint32_t)__popcll(bal));
-        qb = __shfl(qb, leader);
-        if (is_new) qnxt[qb + __popcll(bal & ((1ull << lane_id()) - 1))] = (uint32_t)(base + peer);
-      }
+    const uint32_t pm = valid ? a.mask[p] : 0;
+    const uint32_t pushes = expand_node<ASZP, uint32_t, false>(a, valid, u, a.obkt[o], org, nf, pm, base, d,
+                                                        a.cnt + base, a.hops + base, qnxt, &a.lvl[d + 1], base,
+                                                        overflow);
+    if (valid) {
+      a.egress[p] = (uint8_t)pushes;
+      if (a.record) a.egress_acc[p] += pushes;
     }
-    a.egress[p] = (uint8_t)pushes;
   }
   if (overflow) atomicOr(a.err, ERR_INBOUND);
 }
@@ -447,15 +535,18 @@ static BfsArgs bfs_args(Engine& e) {
   a.nfail = e.nfail; a.mask = e.mask; a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb; a.egress = e.egress;
   a.lvl = e.lvl; a.err = e.err; a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin;
   a.PAIRS = e.PAIRS;
+  a.egress_acc = e.egress_acc; a.stake = e.stake; a.srank = e.srank; a.strand = e.strand; a.bm = e.bm;
+  a.rs_u32 = e.rs_u32; a.rs_ssum = e.rs_ssum; a.rs_hist = e.rs_hist; a.W = e.bm_words; a.record = 0;
   return a;
 }
 
 size_t bfs_wg_lds_bytes(uint32_t N) {
-  return 16 + 4 * (size_t)N + ((N + 3) & ~3u) + 2 * 2 * (size_t)((N + 1) & ~1u);
+  return 64 + 1024 + 4 * (size_t)N + 2 * (size_t)((N + 3) & ~3u) + 2 * 2 * (size_t)((N + 1) & ~1u);
 }
 
-hipError_t launch_bfs(Engine& e) {
+hipError_t launch_bfs(Engine& e, bool record) {
   BfsArgs a = bfs_args(e);
+  a.record = record ? 1 : 0;
   hipError_t r;
   if (e.bfs_mode == GS_BFS_WORKGROUP) {
     const size_t lds = bfs_wg_lds_bytes(e.N);
@@ -503,8 +594,11 @@ struct CpArgs {
   uint8_t* prune_round;
   uint32_t* slot_prunes;
   uint32_t* mask;
+  uint32_t* ingress_acc;
+  uint32_t* prune_acc;
   uint32_t* err;
   uint32_t N, S, ASZ, ASZP, capin;
+  int record;
   size_t PAIRS;
 };
 
@@ -516,141 +610,329 @@ __device__ inline uint64_t min_ingress_stake(uint64_t stake, double thr) {
   return (uint64_t)x;
 }
 
+__device__ inline uint64_t sat_add(uint64_t a, uint64_t b) { return a + b < a ? ~0ull : a + b; }
+
+// prune_connections -> PushActiveSet::prune(prunee u, pruner v, [origin]) for one
+// prunee (gossip.rs:701-737, push_active_set.rs:56-71,143-151): set the prune bit
+// of v's ring slot in u's entry for this origin, if v is still there.
+__device__ inline void apply_prune(const CpArgs& a, uint32_t o, uint32_t ob, uint32_t u, uint32_t v) {
+  if (GS_OOB(u, a.N, a.err, "apply_prune u")) return;
+  const uint32_t b = min((uint32_t)a.bucket[u], ob);
+  const uint32_t ent = u * NB + b;
+  const uint32_t hv = a.hl[ent];
+  const uint32_t head = hv & 0xFF, L = hv >> 8;
+  const uint32_t* row = a.peers + (size_t)ent * a.ASZP;
+  for (uint32_t j = 0; j < L; ++j) {
+    uint32_t slot = head + j;
+    if (slot >= a.ASZ) slot -= a.ASZ;
+    if (row[slot] == v) {
+      atomicOr(&a.mask[(size_t)o * a.N + u], 1u << slot);
+      return;
+    }
+  }
+}
+
+// Maximum of x (< 32) over the wave's ACTIVE lanes, wave-uniform. Built from
+// ballots, which see exactly the active lanes; a shuffle butterfly would read
+// stale registers of lanes switched off by an enclosing divergent branch.
+__device__ inline uint32_t active_max_small(uint32_t x) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t b = 16; b; b >>= 1)
+    if (__ballot(x >= m + b)) m += b;
+  return __builtin_amdgcn_readfirstlane(m);
+}
+
+__device__ inline void cswap(uint32_t& x, uint32_t& y) {
+  const uint32_t lo = min(x, y), hi = max(x, y);
+  x = lo;
+  y = hi;
+}
+
+// Batcher odd-even merge sort of 16 keys (63 comparators), register-resident.
+__device__ inline void sort16(uint32_t (&r)[16]) {
+#pragma unroll
+  for (int p = 1; p < 16; p <<= 1)
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+      for (int j = k % p; j + k < 16; j += 2 * k)
+#pragma unroll
+        for (int i = 0; i < k; ++i)
+          if (i + j + k < 16 && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cswap(r[i + j], r[i + j + k]);
+}
+
+// Generic per-pair path (any in-degree / cache length): state read and written in place.
+template <bool CONSUME, bool PRUNE, bool APPLY>
+__device__ inline void cp_generic(const CpArgs& a, size_t p, uint32_t o, uint32_t v, bool& cache_overflow) {
+  const size_t PAIRS = a.PAIRS;
+  uint32_t meta = a.cmeta[p];
+  uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
+  uint32_t c = 0;
+  if (CONSUME) {
+    // consume_messages (gossip.rs:618-653): inbound sorted by (hop, base58 id) =
+    // ascending record value; ReceivedCache::record with num_dups = rank.
+    c = a.cnt[p];
+    if (c > a.capin) c = a.capin;
+    uint32_t prev = 0;
+    for (uint32_t k = 0; k < c; ++k) {
+      uint32_t best = 0xFFFFFFFFu;
+      for (uint32_t j = 0; j < c; ++j) {
+        const uint32_t r = a.inb[(size_t)j * PAIRS + p];
+        if ((k == 0 || r > prev) && r < best) best = r;
+      }
+      prev = best;
+      const uint32_t src = best & 0xFFFFFFu;
+      if (k == 0) up = up < 255 ? up + 1 : 255;
+      int found = -1;
+      for (uint32_t i = 0; i < len; ++i)
+        if (a.ckey[(size_t)i * PAIRS + p] == src) { found = (int)i; break; }
+      if (k < 2) {
+        if (found >= 0) {
+          uint8_t& sc = a.cscore[(size_t)found * PAIRS + p];
+          const uint32_t s0 = sc & 0x7F;
+          sc = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
+        } else if (len < CACHE_CAP) {
+          a.ckey[(size_t)len * PAIRS + p] = src;
+          a.cscore[(size_t)len * PAIRS + p] = 1;
+          ++len;
+        } else {
+          cache_overflow = true;
+        }
+      } else if (found < 0 && len < CACHE_LIMIT) {
+        a.ckey[(size_t)len * PAIRS + p] = src;
+        a.cscore[(size_t)len * PAIRS + p] = 0;
+        ++len;
+      }
+    }
+    meta = len | (up << 8) | (meta & 0xFF0000u);
+    if (a.record && c) a.ingress_acc[p] += c;
+  }
+  uint32_t plen = (meta >> 16) & 0xFF;
+  if (PRUNE) {
+    // send_prunes -> ReceivedCache::prune (received_cache.rs:38-63,100-131).
+    uint32_t npr = 0;
+    plen = 0;
+    if (up >= MIN_NUM_UPSERTS) {
+      const uint32_t org = a.origin[o];
+      const uint64_t sv = a.stake[v], so = a.stake[org];
+      const uint64_t mis = min_ingress_stake(sv < so ? sv : so, a.thr[o]);
+      const uint32_t mi = a.min_ingress[o];
+      for (uint32_t i = 0; i < len; ++i) {
+        const uint32_t ki = a.ckey[(size_t)i * PAIRS + p];
+        const uint32_t si = a.cscore[(size_t)i * PAIRS + p] & 0x7F;
+        const uint64_t sti = a.stake[ki];
+        uint32_t pos = 0;
+        uint64_t cum = 0;
+        for (uint32_t j = 0; j < len; ++j) {
+          if (j == i) continue;
+          const uint32_t kj = a.ckey[(size_t)j * PAIRS + p];
+          const uint32_t sj = a.cscore[(size_t)j * PAIRS + p] & 0x7F;
+          const uint64_t stj = a.stake[kj];
+          // sort by Reverse((score, stake)); ties by ascending id (canonical order)
+          const bool before = sj > si || (sj == si && (stj > sti || (stj == sti && kj < ki)));
+          if (before) { ++pos; cum = sat_add(cum, stj); }
+        }
+        if (pos >= mi && cum >= mis && ki != org) {
+          a.cscore[(size_t)i * PAIRS + p] = (uint8_t)(si | PRUNED_FLAG);
+          ++npr;
+        }
+      }
+      plen = len;  // std::mem::take: the entry resets, the pruned keys stay readable
+      len = 0;
+      up = 0;
+    }
+    a.prune_round[p] = (uint8_t)(npr < 255 ? npr : 255);
+    if (npr) {
+      atomicAdd(&a.slot_prunes[o], npr);
+      if (a.record) a.prune_acc[p] += npr;
+    }
+    meta = len | (up << 8) | (plen << 16);
+  }
+  if (APPLY && plen) {
+    const uint32_t org = a.origin[o], ob = a.obkt[o];
+    for (uint32_t i = 0; i < plen; ++i) {
+      if (!(a.cscore[(size_t)i * PAIRS + p] & PRUNED_FLAG)) continue;
+      const uint32_t u = a.ckey[(size_t)i * PAIRS + p];
+      if (u != org) apply_prune(a, o, ob, u, v);
+    }
+  }
+  a.cmeta[p] = meta;
+}
+
+// Fused fast path (in-degree <= 16, cache length + in-degree <= 24, the steady
+// state): inbound records sorted in registers by a sorting network, the cache
+// entry held in registers, only changed slots written back.
+constexpr int FC = 16, FL = 16;
+
+__device__ inline void cp_fast(const CpArgs& a, size_t p, uint32_t c, uint32_t meta) {
+  const size_t PAIRS = a.PAIRS;
+  uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
+  if (c == 0) {  // nothing received: only the pruned-len field resets
+    if (meta & 0xFF0000u) a.cmeta[p] = meta & 0xFFFFu;
+    return;
+  }
+  // Row bases (i * PAIRS) are wave-uniform (scalar registers); the lane offset is a
+  // 32-bit pair index. Loads are bounded by the wave's maximum length (a uniform
+  // branch) and issued unconditionally, then masked: no per-load waits.
+  const uint32_t q = (uint32_t)p;
+  const uint32_t wlen = active_max_small(len);
+  uint32_t key[FL], sc[FL];
+#pragma unroll
+  for (int i = 0; i < FL; ++i) {
+    key[i] = 0xFFFFFFFFu;
+    sc[i] = 0;
+    if ((uint32_t)i < wlen) {
+      key[i] = (a.ckey + (size_t)i * PAIRS)[q];
+      sc[i] = (a.cscore + (size_t)i * PAIRS)[q];
+    }
+  }
+  asm volatile("" ::: "memory");  // keep the loads above: one wait for all of them
+#ifdef GS_DEBUG_BOUNDS
+  for (int i = 0; i < FL; ++i)
+    if ((uint32_t)i < len && GS_OOB(key[i], a.N, a.err, "cp_fast cached key")) return;
+  if (GS_OOB(p, PAIRS, a.err, "cp_fast p")) return;
+#endif
+#pragma unroll
+  for (int i = 0; i < FL; ++i) {
+    const bool in = (uint32_t)i < len;
+    key[i] = in ? key[i] : 0xFFFFFFFFu;
+    sc[i] = in ? sc[i] : 0u;  // live entries never carry the pruned flag (set only as len resets)
+  }
+  uint32_t dirty = 0;
+  if (c) {
+    uint32_t r[FC];
+    const uint32_t wc = active_max_small(c);
+#pragma unroll
+    for (int j = 0; j < FC; ++j) {
+      r[j] = 0xFFFFFFFFu;
+      if ((uint32_t)j < wc) r[j] = (a.inb + (size_t)j * PAIRS)[q];
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < FC; ++j) r[j] = (uint32_t)j < c ? r[j] : 0xFFFFFFFFu;
+#ifdef GS_DEBUG_BOUNDS
+    for (int j = 0; j < FC; ++j)
+      if ((uint32_t)j < c && GS_OOB(r[j] & 0xFFFFFFu, a.N, a.err, "cp_fast record src")) return;
+#endif
+    sort16(r);
+    up = up < 255 ? up + 1 : 255;  // rank 0 (received_cache.rs:84-86)
+#pragma unroll
+    for (int k = 0; k < FC; ++k) {
+      if ((uint32_t)k >= c) break;
+      const uint32_t src = r[k] & 0xFFFFFFu;
+      uint32_t fm = 0;
+#pragma unroll
+      for (int i = 0; i < FL; ++i) fm |= (uint32_t)(key[i] == src) << i;
+      if (k < 2) {  // timely: score += 1, inserted regardless of the 50-key cap
+        if (fm) {
+#pragma unroll
+          for (int i = 0; i < FL; ++i)
+            if ((fm >> i) & 1u) sc[i] = sc[i] < 0x7F ? sc[i] + 1 : 0x7F;
+          dirty |= fm;
+        } else {
+#pragma unroll
+          for (int i = 0; i < FL; ++i)
+            if ((uint32_t)i == len) { key[i] = src; sc[i] = 1; }
+          dirty |= 1u << len;
+          ++len;
+        }
+      } else if (!fm && len < CACHE_LIMIT) {
+#pragma unroll
+        for (int i = 0; i < FL; ++i)
+          if ((uint32_t)i == len) { key[i] = src; sc[i] = 0; }
+        dirty |= 1u << len;
+        ++len;
+      }
+    }
+    if (a.record) a.ingress_acc[p] += c;
+  }
+#pragma unroll
+  for (int i = 0; i < FL; ++i)
+    if ((dirty >> i) & 1u) {
+      (a.ckey + (size_t)i * PAIRS)[q] = key[i];
+      (a.cscore + (size_t)i * PAIRS)[q] = (uint8_t)sc[i];
+    }
+  a.cmeta[p] = len | (up << 8);
+}
+
+// Step-wise forms (gs_consume_messages / gs_send_prunes / gs_prune_connections).
 template <bool CONSUME, bool PRUNE, bool APPLY>
 __global__ __launch_bounds__(256) void k_consume_prune(CpArgs a) {
-  const size_t PAIRS = a.PAIRS;
   bool cache_overflow = false;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < PAIRS; p += (size_t)gridDim.x * blockDim.x) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.PAIRS; p += (size_t)gridDim.x * blockDim.x) {
     const uint32_t o = (uint32_t)(p / a.N);
     const uint32_t v = (uint32_t)(p - (size_t)o * a.N);
-    uint32_t meta = a.cmeta[p];
-    uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
-    if (CONSUME) {
-      // consume_messages (gossip.rs:618-653): inbound sorted by (hop, base58 id) =
-      // ascending record value; ReceivedCache::record with num_dups = rank.
-      uint32_t c = a.cnt[p];
-      if (c > a.capin) c = a.capin;
-      if (c) {
-        uint32_t prev = 0;
-        for (uint32_t k = 0; k < c; ++k) {
-          uint32_t best = 0xFFFFFFFFu;
-          for (uint32_t j = 0; j < c; ++j) {
-            const uint32_t r = a.inb[(size_t)j * PAIRS + p];
-            if ((k == 0 || r > prev) && r < best) best = r;
-          }
-          prev = best;
-          const uint32_t src = best & 0xFFFFFFu;
-          if (k == 0) up = up < 255 ? up + 1 : 255;
-          int found = -1;
-          for (uint32_t i = 0; i < len; ++i)
-            if (a.ckey[(size_t)i * PAIRS + p] == src) { found = (int)i; break; }
-          if (k < 2) {
-            if (found >= 0) {
-              uint8_t& sc = a.cscore[(size_t)found * PAIRS + p];
-              const uint32_t s0 = sc & 0x7F;
-              sc = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
-            } else if (len < CACHE_CAP) {
-              a.ckey[(size_t)len * PAIRS + p] = src;
-              a.cscore[(size_t)len * PAIRS + p] = 1;
-              ++len;
-            } else {
-              cache_overflow = true;
-            }
-          } else if (found < 0 && len < CACHE_LIMIT) {
-            a.ckey[(size_t)len * PAIRS + p] = src;
-            a.cscore[(size_t)len * PAIRS + p] = 0;
-            ++len;
-          }
-        }
-      }
-      meta = len | (up << 8) | (meta & 0xFF0000u);
-    }
-    uint32_t plen = (meta >> 16) & 0xFF;
-    if (PRUNE) {
-      // send_prunes -> ReceivedCache::prune (received_cache.rs:38-63,100-131).
-      uint32_t npr = 0;
-      plen = 0;
-      if (up >= MIN_NUM_UPSERTS) {
-        const uint32_t org = a.origin[o];
-        const uint64_t sv = a.stake[v], so = a.stake[org];
-        const uint64_t mis = min_ingress_stake(sv < so ? sv : so, a.thr[o]);
-        const uint32_t mi = a.min_ingress[o];
-        for (uint32_t i = 0; i < len; ++i) {
-          const uint32_t ki = a.ckey[(size_t)i * PAIRS + p];
-          const uint32_t si = a.cscore[(size_t)i * PAIRS + p] & 0x7F;
-          const uint64_t sti = a.stake[ki];
-          uint32_t pos = 0;
-          uint64_t cum = 0;
-          for (uint32_t j = 0; j < len; ++j) {
-            if (j == i) continue;
-            const uint32_t kj = a.ckey[(size_t)j * PAIRS + p];
-            const uint32_t sj = a.cscore[(size_t)j * PAIRS + p] & 0x7F;
-            const uint64_t stj = a.stake[kj];
-            // sort by Reverse((score, stake)); ties by ascending id (canonical order)
-            const bool before = sj > si || (sj == si && (stj > sti || (stj == sti && kj < ki)));
-            if (before) {
-              ++pos;
-              cum = cum + stj < cum ? ~0ull : cum + stj;
-            }
-          }
-          const bool pruned = pos >= mi && cum >= mis && ki != org;
-          if (pruned) {
-            a.cscore[(size_t)i * PAIRS + p] = (uint8_t)(si | PRUNED_FLAG);
-            ++npr;
-          }
-        }
-        plen = len;  // std::mem::take: the entry resets, the pruned keys stay readable
-        len = 0;
-        up = 0;
-      }
-      a.prune_round[p] = (uint8_t)(npr < 255 ? npr : 255);
-      if (npr) atomicAdd(&a.slot_prunes[o], npr);
-      meta = len | (up << 8) | (plen << 16);
-    }
-    if (APPLY && plen) {
-      // prune_connections -> PushActiveSet::prune(prunee, pruner = v, [origin])
-      // (gossip.rs:701-737, push_active_set.rs:56-71,143-151).
-      const uint32_t org = a.origin[o];
-      const uint32_t ob = a.obkt[o];
-      for (uint32_t i = 0; i < plen; ++i) {
-        const uint8_t sc = a.cscore[(size_t)i * PAIRS + p];
-        if (!(sc & PRUNED_FLAG)) continue;
-        const uint32_t u = a.ckey[(size_t)i * PAIRS + p];
-        if (u == org) continue;
-        const uint32_t b = min((uint32_t)a.bucket[u], ob);
-        const uint32_t ent = u * NB + b;
-        const uint32_t hv = a.hl[ent];
-        const uint32_t head = hv & 0xFF, L = hv >> 8;
-        const uint32_t* row = a.peers + (size_t)ent * a.ASZP;
-        for (uint32_t j = 0; j < L; ++j) {
-          uint32_t slot = head + j;
-          if (slot >= a.ASZ) slot -= a.ASZ;
-          if (row[slot] == v) {
-            atomicOr(&a.mask[(size_t)o * a.N + u], 1u << slot);
-            break;
-          }
-        }
-      }
-    }
-    a.cmeta[p] = meta;
+    cp_generic<CONSUME, PRUNE, APPLY>(a, p, o, v, cache_overflow);
   }
   if (cache_overflow) atomicOr(a.err, ERR_CACHE);
 }
 
-hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply) {
+// Fused round, kernel 1: consume every pair (register fast path when the inbound
+// list and the cache entry fit), then queue the pairs whose prune is due.
+__global__ __launch_bounds__(256) void k_consume_fused(CpArgs a, uint32_t* __restrict__ work,
+                                                       uint32_t* __restrict__ work_count) {
+  bool cache_overflow = false;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.PAIRS; p += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t meta = a.cmeta[p];
+    uint32_t c = a.cnt[p];
+    if (c > a.capin) c = a.capin;
+    if (c <= (uint32_t)FC && (meta & 0xFF) + c <= (uint32_t)FL) {
+      cp_fast(a, p, c, meta);
+    } else {
+      const uint32_t o = (uint32_t)(p / a.N);
+      cp_generic<true, false, false>(a, p, o, (uint32_t)(p - (size_t)o * a.N), cache_overflow);
+    }
+    const uint32_t m2 = a.cmeta[p];
+    const bool due = ((m2 >> 8) & 0xFF) >= MIN_NUM_UPSERTS;
+    if (!due) {  // send_prunes yields nothing for this pair this round
+      a.prune_round[p] = 0;
+      if (m2 & 0xFF0000u) a.cmeta[p] = m2 & 0xFFFFu;
+    }
+    const unsigned long long bal = __ballot(due);
+    if (bal) {
+      const int leader = __ffsll((long long)bal) - 1;
+      uint32_t base = 0;
+      if ((int)lane_id() == leader) base = atomicAdd(work_count, (uint32_t)__popcll(bal));
+      base = __shfl(base, leader);
+      if (due) work[base + __popcll(bal & ((1ull << lane_id()) - 1))] = (uint32_t)p;
+    }
+  }
+  if (cache_overflow) atomicOr(a.err, ERR_CACHE);
+}
+
+// Fused round, kernel 2: send_prunes + prune_connections for the queued pairs only.
+__global__ __launch_bounds__(256) void k_prune_fused(CpArgs a, const uint32_t* __restrict__ work,
+                                                     const uint32_t* __restrict__ work_count) {
+  bool cache_overflow = false;
+  const uint32_t n = *work_count;
+  if (GS_OOB(n, a.PAIRS + 1, a.err, "prune work count")) return;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const size_t p = work[i];
+    if (GS_OOB(p, a.PAIRS, a.err, "prune work pair")) continue;
+    const uint32_t o = (uint32_t)(p / a.N);
+    cp_generic<false, true, true>(a, p, o, (uint32_t)(p - (size_t)o * a.N), cache_overflow);
+  }
+}
+
+hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record) {
   CpArgs a;
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
   a.min_ingress = e.min_ingress; a.thr = e.thr; a.cnt = e.cnt; a.inb = e.inb; a.cmeta = e.cmeta; a.ckey = e.ckey;
   a.cscore = e.cscore; a.prune_round = e.prune_round; a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.err = e.err;
+  a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc; a.record = record ? 1 : 0;
   a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.ASZP = e.ASZP; a.capin = e.capin; a.PAIRS = e.PAIRS;
   const uint32_t grid = grid_for(e.PAIRS, 256, 8192);
-  if (prune) {
-    hipError_t r = hipMemsetAsync(e.slot_prunes, 0, e.S * 4, e.st);
-    if (r != hipSuccess) return r;
+  hipError_t r;
+  if (prune && (r = hipMemsetAsync(e.slot_prunes, 0, e.S * 4, e.st)) != hipSuccess) return r;
+  if (consume && prune && apply) {
+    if ((r = hipMemsetAsync(e.work_count, 0, 4, e.st)) != hipSuccess) return r;
+    hipLaunchKernelGGL(k_consume_fused, dim3(grid), dim3(256), 0, e.st, a, e.work, e.work_count);
+    hipLaunchKernelGGL(k_prune_fused, dim3(grid), dim3(256), 0, e.st, a, e.work, e.work_count);
+    return hipGetLastError();
   }
 #define GS_CP(C, P, A) hipLaunchKernelGGL((k_consume_prune<C, P, A>), dim3(grid), dim3(256), 0, e.st, a)
-  if (consume && prune && apply) GS_CP(true, true, true);
-  else if (consume && !prune && !apply) GS_CP(true, false, false);
+  if (consume && !prune && !apply) GS_CP(true, false, false);
   else if (!consume && prune && !apply) GS_CP(false, true, false);
   else if (!consume && !prune && apply) GS_CP(false, false, true);
   else return hipErrorInvalidValue;
@@ -683,6 +965,9 @@ struct StatsArgs {
   uint32_t N, S, W;
 };
 
+// FULL: the step-wise gs_record_round (reads the per-round counters of every pair);
+// LITE: after a fused round whose kernels already accumulated egress/ingress/prunes.
+template <bool FULL>
 __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
   const uint32_t o = blockIdx.y;
   const size_t base = (size_t)o * a.N;
@@ -701,12 +986,14 @@ __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
     const uint32_t hh = a.hops[p];
     const uint32_t c = a.cnt[p];
     pushes += c;
-    a.ingress_acc[p] += c;
-    a.prune_acc[p] += a.prune_round[p];
+    if (FULL) {
+      a.ingress_acc[p] += c;
+      a.prune_acc[p] += a.prune_round[p];
+    }
     if (hh != 0xFF) {
       ++vis;
       atomicAdd(&h[hh], 1u);
-      a.egress_acc[p] += a.egress[p];
+      if (FULL) a.egress_acc[p] += a.egress[p];
     } else if (!(nf && a.frank[v] < nf)) {
       a.strand[p] += 1;
       ++sc;
@@ -817,7 +1104,9 @@ __global__ __launch_bounds__(256) void k_stats_finalize(StatsArgs a, uint32_t re
   }
 }
 
-hipError_t launch_stats(Engine& e, uint32_t rec_slot) {
+// mode 0: full pass; 1: hop-only pass (fused level-synchronous round); 2: finalize only
+// (the workgroup BFS already reduced the round).
+hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   StatsArgs a;
   a.stake = e.stake; a.frank = e.frank; a.srank = e.srank; a.by_srank = e.by_srank; a.nfail = e.nfail;
   a.hops = e.hops; a.cnt = e.cnt; a.egress = e.egress; a.prune_round = e.prune_round; a.slot_prunes = e.slot_prunes;
@@ -825,7 +1114,8 @@ hipError_t launch_stats(Engine& e, uint32_t rec_slot) {
   a.rs_u32 = e.rs_u32; a.rs_ssum = e.rs_ssum; a.rs_hist = e.rs_hist; a.hist_acc = e.hist_acc; a.bm = e.bm;
   a.sum = e.sum; a.N = e.N; a.S = e.S; a.W = e.bm_words;
   uint32_t gx = grid_for(e.N, 256, 64);
-  hipLaunchKernelGGL(k_stats_pass, dim3(gx, e.S), dim3(256), 0, e.st, a);
+  if (mode == 0) hipLaunchKernelGGL(k_stats_pass<true>, dim3(gx, e.S), dim3(256), 0, e.st, a);
+  else if (mode == 1) hipLaunchKernelGGL(k_stats_pass<false>, dim3(gx, e.S), dim3(256), 0, e.st, a);
   hipLaunchKernelGGL(k_stats_finalize, dim3(e.S), dim3(256), 0, e.st, a, rec_slot);
   return hipGetLastError();
 }

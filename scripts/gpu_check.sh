@@ -12,6 +12,9 @@ step() {  # step <name> <seconds> <cmd...>
   echo "== $name exit $rc"
   tail -n 25 "gpurun_out/$name.log"
   if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  if grep -qiE "illegal memory access|memory access fault|hipErrorLaunchFailure|GPU fault|HSA_STATUS_ERROR" "gpurun_out/$name.log"; then
+    echo "stopping after $name: GPU fault signature in the log"; exit 99
+  fi
   return 0
 }
 MODE=${1:-all}
