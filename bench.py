@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--split-round", action="store_true", help="step kernels instead of the one-kernel round")
     args = ap.parse_args()
 
     gs = load_pkg()          # loads libgossip_hip.so (and its HIP runtime) before torch, if torch is used at all
@@ -116,7 +117,7 @@ def main():
     S = args.slots or args.nodes
     eng = gs.Engine(stakes, S, fanout=args.fanout, active_set_size=args.active_set_size,
                     rotation_probability=args.rotation_probability, seed=args.seed + rank, device=local_rank,
-                    bfs_mode=args.bfs_mode, profile=not args.no_profile)
+                    bfs_mode=args.bfs_mode, profile=not args.no_profile, split_round=args.split_round)
     origins = [s % args.nodes for s in range(S)]
     eng.set_slots(origins, args.min_ingress, args.threshold)
     eng.init_active_sets()
@@ -136,19 +137,33 @@ def main():
     assert summ.shape[0] == args.steps
     E = float(summ["pushes"].astype("float64").sum())
     V = float(summ["visited"].astype("float64").sum())
-    bfs_ms, bfs_n = eng.kernel_time("bfs")
+    fused = eng.info()["fused_round"]
+    k_ms, k_n = eng.kernel_time("round" if fused else "bfs")
     dt = reduce(dt_local, lambda d: d.ReduceOp.MAX)
     E_all = reduce(E, lambda d: d.ReduceOp.SUM)
     asz = args.active_set_size
-    b_prop = V * (4 * asz + 5) + 8 * E  # this rank's algorithmic propagation bytes over the timed steps
+    # SURVEY.md 8(d) algorithmic bytes of this rank's timed steps:
+    #   propagation  B_prop    = V*(4*ASZ + 5) + 8*E
+    #   consume      B_consume = 5*E + 16*R        (R = receiving pairs = V - origins)
+    #   statistics   B_stats   = 8 per (origin, node)
+    b_prop = V * (4 * asz + 5) + 8 * E
+    R = V - S * args.steps
+    b_round = b_prop + 5 * E + 16 * R + 8.0 * args.nodes * S * args.steps
+    b_kernel = b_round if fused else b_prop
     roof = None
-    if bfs_ms > 0:
-        achieved = b_prop / (bfs_ms * 1e-3) / 1e9
+    if k_ms > 0:
+        achieved = b_kernel / (k_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "k_bfs_wg" if eng.info()["bfs_mode"] == gs.GS_BFS_WORKGROUP else "k_bfs_level",
-                "bytes_per_launch": round(b_prop / max(bfs_n, 1)), "avg_launch_us": round(bfs_ms * 1e3 / max(bfs_n, 1), 2),
-                "launches": bfs_n}
+                "kernel": "k_round_wg" if fused else
+                          ("k_bfs_wg" if eng.info()["bfs_mode"] == gs.GS_BFS_WORKGROUP else "k_bfs_level"),
+                "bytes_model": "B_prop+B_consume+B_stats (SURVEY 8d)" if fused else "B_prop (SURVEY 8d)",
+                "bytes_per_launch": round(b_kernel / max(k_n, 1)), "avg_launch_us": round(k_ms * 1e3 / max(k_n, 1), 2),
+                "launches": k_n}
+    phases = None
+    if os.environ.get("GS_PHASE_PROFILE") == "1" and fused:  # workgroup-ms per k_round_wg phase
+        names = ["init", "bfs", "csr_stats", "consume_prune", "heavy", "summary"]
+        phases = {nm: round(eng.kernel_time("phase." + chr(65 + i))[0], 2) for i, nm in enumerate(names)}
     out = {
         "metric": METRIC,
         "value": E_all / dt,
@@ -166,9 +181,11 @@ def main():
                    "nodes": args.nodes, "origin_slots_per_gpu": S, "push_fanout": args.fanout,
                    "active_set_size": asz, "rotation_probability": args.rotation_probability,
                    "prune_stake_threshold": args.threshold, "min_ingress_nodes": args.min_ingress,
-                   "bfs_mode": eng.info()["bfs_mode"], "parallelism": f"origin-sharded x{world}"},
+                   "bfs_mode": eng.info()["bfs_mode"], "fused_round": fused,
+                   "parallelism": f"origin-sharded x{world}"},
         "origin_rounds_per_s": S * args.steps * world / dt,
         "roofline": roof,
+        **({"phases_wg_ms": phases} if phases else {}),
         "cpu_baseline": None,
     }
     eng.close()

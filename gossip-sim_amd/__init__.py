@@ -21,6 +21,8 @@ LIB_PATH = os.path.join(PKG_DIR, "libgossip_hip.so")
 
 GS_BFS_AUTO, GS_BFS_WORKGROUP, GS_BFS_LEVEL = 0, 1, 2
 GS_FLAG_PROFILE = 1
+GS_FLAG_SPLIT_ROUND = 2
+GS_FLAG_NARROW_WAVE_PATH = 4
 HOP_UNREACHED = 0xFF
 B58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
 
@@ -99,6 +101,7 @@ EXPORTS = {
     "gs_read_failed": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "gs_kernel_time": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "gs_kernel_time_reset": (C.c_int, [C.c_void_p]),
+    "gs_engine_round_kind": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "gs_engine_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_uint64)]),
     "gs_hops_stat_new": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p]),
@@ -166,14 +169,16 @@ class Engine:
     """One engine = one device + one shared active-set trajectory + n_slots sims."""
 
     def __init__(self, stakes, n_slots, *, fanout=6, active_set_size=12, rotation_probability=0.013333, seed=0,
-                 device=0, bfs_mode=GS_BFS_AUTO, inbound_capacity=0, profile=False):
+                 device=0, bfs_mode=GS_BFS_AUTO, inbound_capacity=0, profile=False, split_round=False,
+                 narrow_wave_path=False):
         L = lib()
         self.stakes = np.ascontiguousarray(stakes, dtype=np.uint64)
         self.n = len(self.stakes)
         self.n_slots = n_slots
         self.active_set_size = active_set_size
         p = Params(fanout, active_set_size, rotation_probability, seed, device, bfs_mode, inbound_capacity,
-                   GS_FLAG_PROFILE if profile else 0)
+                   (GS_FLAG_PROFILE if profile else 0) | (GS_FLAG_SPLIT_ROUND if split_round else 0) |
+                   (GS_FLAG_NARROW_WAVE_PATH if narrow_wave_path else 0))
         h = C.c_void_p()
         _check(L.gs_create(C.byref(p), _ptr(self.stakes), self.n, n_slots, C.byref(h)))
         self.h = h
@@ -189,7 +194,10 @@ class Engine:
     def info(self):
         n, s, m, b = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint64()
         _check(lib().gs_engine_info(self.h, C.byref(n), C.byref(s), C.byref(m), C.byref(b)))
-        return {"n_nodes": n.value, "n_slots": s.value, "bfs_mode": m.value, "device_bytes": b.value}
+        f = C.c_uint32()
+        _check(lib().gs_engine_round_kind(self.h, C.byref(f)))
+        return {"n_nodes": n.value, "n_slots": s.value, "bfs_mode": m.value, "device_bytes": b.value,
+                "fused_round": bool(f.value)}
 
     def set_slots(self, origins, min_ingress=2, thresholds=0.15):
         S = self.n_slots

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -12,10 +13,6 @@
 #include "gs_internal.h"
 
 using namespace gs;
-
-namespace gs {
-size_t bfs_wg_lds_bytes(uint32_t N);
-}
 
 static thread_local std::string g_err;
 
@@ -144,6 +141,7 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   e->ASZ = prm->active_set_size;
   e->ASZP = (e->ASZ + 3) & ~3u;
   e->fanout = prm->push_fanout;
+  e->fcap = std::min(e->fanout, e->ASZ);
   e->capin = prm->inbound_capacity ? prm->inbound_capacity : 64;
   if (hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) {
     destroy_engine(e);
@@ -161,6 +159,9 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   }
   if (mode != GS_BFS_WORKGROUP && mode != GS_BFS_LEVEL) { destroy_engine(e); return fail(GS_EINVAL, "bfs_mode"); }
   e->bfs_mode = mode;
+  // one-kernel round (gs_round): per-slot state in LDS, at most 160 KiB per workgroup
+  e->fused = mode == GS_BFS_WORKGROUP && !(prm->flags & GS_FLAG_SPLIT_ROUND) &&
+             round_wg_lds_bytes(n, e->fcap, e->ASZP) <= 160 * 1024;
 
   const size_t N = n, S = n_slots, PAIRS = e->PAIRS;
   ALLOC(e->stake, N, 0);
@@ -171,6 +172,9 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   ALLOC(e->frank, N, 0);
   ALLOC(e->srank, N, 0);
   ALLOC(e->by_srank, N, 0);
+  ALLOC(e->prank, N, 0);
+  ALLOC(e->by_prank, N, 0);
+  ALLOC(e->pstake, N, 0);
   ALLOC(e->origin, S, 0);
   ALLOC(e->obkt, S, 0);
   ALLOC(e->min_ingress, S, 0);
@@ -209,6 +213,7 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   e->sum_cap = 64;
   ALLOC(e->sum, (size_t)e->sum_cap * S, 0);
   ALLOC(e->err, 4, 0);
+  if (const char* pp = std::getenv("GS_PHASE_PROFILE"); pp && pp[0] == '1') ALLOC(e->phase_clk, 8, 0);
 
   // stakes, buckets and the static rotation prefix sums
   std::vector<uint8_t> b(N);
@@ -225,6 +230,21 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   if (launch_scatter_rank(*e, e->by_srank, e->srank) != hipSuccess) {
     destroy_engine(e);
     return fail(GS_EHIP, "stake-rank scatter");
+  }
+  // prune rank: (stake desc, id asc) -- the order ReceivedCache::prune sorts by, ties canonical
+  {
+    std::vector<uint32_t> ids(N), pr(N);
+    std::vector<uint64_t> ps(N);
+    for (uint32_t i = 0; i < n; ++i) ids[i] = i;
+    std::stable_sort(ids.begin(), ids.end(), [&](uint32_t x, uint32_t y) { return stakes[x] > stakes[y]; });
+    for (uint32_t r = 0; r < n; ++r) { pr[ids[r]] = r; ps[r] = stakes[ids[r]]; }
+    if (hipMemcpyAsync(e->prank, pr.data(), N * 4, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+        hipMemcpyAsync(e->by_prank, ids.data(), N * 4, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+        hipMemcpyAsync(e->pstake, ps.data(), N * 8, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+        hipStreamSynchronize(e->st) != hipSuccess) {
+      destroy_engine(e);
+      return fail(GS_EHIP, "prune-rank upload");
+    }
   }
   if (hipStreamSynchronize(e->st) != hipSuccess) { destroy_engine(e); return fail(GS_EHIP, "create sync"); }
   *out = reinterpret_cast<gs_engine*>(e);
@@ -375,6 +395,7 @@ static int do_bfs(Engine* e, bool record) {
   e->tbegin("bfs", &t0);
   hipError_t r = launch_bfs(*e, record);
   e->tend("bfs", t0);
+  e->inb_valid = true;
   if (r == hipErrorNotSupported) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
   HIPC(r);
   return GS_OK;
@@ -441,6 +462,17 @@ int gs_round(gs_engine* eh, uint32_t round, int record) {
   ENGINE(eh);
   if (int s = need_slots(e)) return s;
   const bool rec = record != 0;
+  if (e->fused) {  // BFS + consume + prune + statistics in one kernel per slot
+    hipEvent_t t0;
+    e->tbegin("round", &t0);
+    hipError_t r = launch_round_wg(*e, rec, e->sum_used);
+    e->tend("round", t0);
+    HIPC(r);
+    e->inb_valid = false;
+    if (int s = gs_chance_to_rotate(eh, round)) return s;
+    if (rec && ++e->sum_used == e->sum_cap) return drain_summaries(e);
+    return GS_OK;
+  }
   if (int s = do_bfs(e, rec)) return s;
   if (int s = do_cp(e, true, true, true, rec)) return s;
   if (int s = gs_chance_to_rotate(eh, round)) return s;
@@ -465,6 +497,9 @@ int gs_read_inbound(gs_engine* eh, uint32_t slot, uint32_t* off, uint32_t* src, 
   ENGINE(eh);
   SLOT_CHECK(slot);
   if (int s = check_err(e)) return s;
+  if (!e->inb_valid)
+    return fail(GS_ESTATE, "inbound records are kept on-chip by the one-kernel gs_round; "
+                           "call gs_run_gossip to materialize them");
   const size_t N = e->N, base = (size_t)slot * N;
   std::vector<uint32_t> cnt(N), recs(N * e->capin);
   HIPC(hipMemcpyAsync(cnt.data(), e->cnt + base, N * 4, hipMemcpyDeviceToHost, e->st));
@@ -706,6 +741,17 @@ int gs_read_failed(gs_engine* eh, uint32_t slot, uint8_t* failed) {
 int gs_kernel_time(gs_engine* eh, const char* family, double* ms, uint64_t* launches) {
   ENGINE(eh);
   HIPC(hipStreamSynchronize(e->st));
+  if (family && std::strncmp(family, "phase.", 6) == 0) {  // workgroup-ms per round-kernel phase (100 MHz clock)
+    *ms = 0;
+    *launches = 0;
+    const int ph = family[6] - 'A';
+    if (!e->phase_clk || ph < 0 || ph >= 8) return GS_OK;
+    unsigned long long v[8];
+    HIPC(hipMemcpy(v, e->phase_clk, sizeof(v), hipMemcpyDeviceToHost));
+    *ms = (double)v[ph] * 1e-5;
+    *launches = e->timers["round"].n;
+    return GS_OK;
+  }
   auto it = e->timers.find(family ? family : "");
   *ms = 0;
   *launches = 0;
@@ -734,6 +780,14 @@ int gs_kernel_time_reset(gs_engine* eh) {
     kv.second.ms = 0;
     kv.second.n = 0;
   }
+  if (e->phase_clk) HIPC(hipMemsetAsync(e->phase_clk, 0, 64, e->st));
+  return GS_OK;
+}
+
+int gs_engine_round_kind(gs_engine* eh, uint32_t* fused) {
+  ENGINE(eh);
+  if (!fused) return fail(GS_EINVAL, "null argument");
+  *fused = e->fused ? 1u : 0u;
   return GS_OK;
 }
 

@@ -26,6 +26,9 @@ struct Engine {
   size_t PAIRS = 0;
   uint32_t ASZ = 0, ASZP = 0, fanout = 0, capin = 64;
   uint32_t bfs_mode = GS_BFS_LEVEL;
+  uint32_t fcap = 0;             // min(fanout, active_set_size): pushes per node
+  bool fused = false;            // gs_round runs the one-kernel workgroup round
+  bool inb_valid = true;         // inbound records materialized in HBM (step-wise BFS)
   hipStream_t st = nullptr;
   size_t dev_bytes = 0;
   std::vector<void*> allocs;
@@ -39,6 +42,9 @@ struct Engine {
   uint32_t* frank = nullptr;
   uint32_t* srank = nullptr;
   uint32_t* by_srank = nullptr;
+  uint32_t* prank = nullptr;     // rank by (stake desc, id asc): prune-order key
+  uint32_t* by_prank = nullptr;
+  uint64_t* pstake = nullptr;    // stake by prune rank
   // slot arrays
   uint32_t* origin = nullptr;
   uint8_t* obkt = nullptr;
@@ -82,6 +88,7 @@ struct Engine {
   std::vector<gs_round_summary> h_sum;  // drained summaries
   uint32_t* err = nullptr;
   uint32_t* h_err = nullptr;  // pinned
+  unsigned long long* phase_clk = nullptr;  // GS_PHASE_PROFILE=1: per-phase workgroup clock sums
 
   std::vector<gs_slot> slots;
   bool slots_set = false, failed_ranked = false;
@@ -93,7 +100,20 @@ struct Engine {
   void tend(const char* fam, hipEvent_t a);
 };
 
-// launchers (gs_kernels.hip); all enqueue on e.st and return hipError_t
+#define GS_ASZP_DISPATCH(ASZP_VAL, CALL)          \
+  switch (ASZP_VAL) {                             \
+    case 4: { constexpr int A = 4; CALL; } break; \
+    case 8: { constexpr int A = 8; CALL; } break; \
+    case 12: { constexpr int A = 12; CALL; } break; \
+    case 16: { constexpr int A = 16; CALL; } break; \
+    case 20: { constexpr int A = 20; CALL; } break; \
+    case 24: { constexpr int A = 24; CALL; } break; \
+    case 28: { constexpr int A = 28; CALL; } break; \
+    case 32: { constexpr int A = 32; CALL; } break; \
+    default: return hipErrorInvalidValue;         \
+  }
+
+// launchers (gs_kernels.hip, gs_round_wg.hip); all enqueue on e.st and return hipError_t
 hipError_t launch_prefix_weights(Engine& e);
 hipError_t launch_init_entries(Engine& e);
 hipError_t launch_fail_keys(Engine& e, uint64_t* keys, uint32_t* ids);
@@ -103,6 +123,9 @@ hipError_t launch_bfs(Engine& e, bool record);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
 hipError_t launch_rotate(Engine& e, uint32_t round);
 hipError_t launch_stats(Engine& e, uint32_t rec_index, int mode);
+hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_index);
+size_t round_wg_lds_bytes(uint32_t N, uint32_t fcap, uint32_t ASZP);
+size_t bfs_wg_lds_bytes(uint32_t N);
 hipError_t launch_gather_strided_u32(Engine& e, const uint32_t* src, size_t stride, uint32_t n, uint32_t* dst);
 hipError_t launch_gather_strided_u8(Engine& e, const uint8_t* src, size_t stride, uint32_t n, uint8_t* dst);
 

@@ -92,19 +92,6 @@ __global__ __launch_bounds__(256) void k_init_entries(const uint8_t* __restrict_
   hl[gid] = (uint16_t)(filled << 8);
 }
 
-#define GS_ASZP_DISPATCH(ASZP_VAL, CALL)          \
-  switch (ASZP_VAL) {                             \
-    case 4: { constexpr int A = 4; CALL; } break; \
-    case 8: { constexpr int A = 8; CALL; } break; \
-    case 12: { constexpr int A = 12; CALL; } break; \
-    case 16: { constexpr int A = 16; CALL; } break; \
-    case 20: { constexpr int A = 20; CALL; } break; \
-    case 24: { constexpr int A = 24; CALL; } break; \
-    case 28: { constexpr int A = 28; CALL; } break; \
-    case 32: { constexpr int A = 32; CALL; } break; \
-    default: return hipErrorInvalidValue;         \
-  }
-
 hipError_t launch_init_entries(Engine& e) {
   const uint32_t total = e.N * NB;
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_init_entries<A>, dim3(grid_for(total, 256)), dim3(256), 0, e.st,
@@ -276,56 +263,6 @@ struct BfsArgs {
   size_t PAIRS;
 };
 
-template <int ASZP>
-__device__ inline void load_row(const uint32_t* __restrict__ src, uint32_t (&row)[ASZP]) {
-  const uint4* s4 = reinterpret_cast<const uint4*>(src);
-#pragma unroll
-  for (int q = 0; q < ASZP / 4; ++q) {
-    const uint4 x = s4[q];
-    row[4 * q] = x.x; row[4 * q + 1] = x.y; row[4 * q + 2] = x.z; row[4 * q + 3] = x.w;
-  }
-}
-
-// PushActiveSet::get_nodes(..).take(fanout) (gossip.rs:527-536, push_active_set.rs:128-141):
-// the first `fanout` peers in FIFO order whose filter lacks the origin -- i.e.
-// not pruned for this slot and not the origin itself. Returns physical ring slots.
-template <int ASZP>
-__device__ inline uint32_t taken_slots(const uint32_t (&row)[ASZP], uint32_t head, uint32_t len, uint32_t S,
-                                       uint32_t pmask, uint32_t origin, uint32_t fanout) {
-  uint32_t elig = 0;
-#pragma unroll
-  for (int s = 0; s < ASZP; ++s) {
-    const uint32_t pos = (uint32_t)s >= head ? (uint32_t)s - head : (uint32_t)s + S - head;
-    const bool ok = (uint32_t)s < S && pos < len && !((pmask >> s) & 1u) && row[s] != origin;
-    elig |= (uint32_t)ok << s;
-  }
-  const uint64_t full = (S == 64) ? ~0ull : ((1ull << S) - 1);
-  const uint64_t e64 = elig;
-  uint64_t fifo = ((e64 >> head) | (e64 << (S - head))) & full;
-  if ((uint32_t)__popcll(fifo) > fanout) {
-    uint64_t sel = 0;
-    for (uint32_t t = 0; t < fanout; ++t) {
-      const uint64_t low = fifo & (~fifo + 1);
-      sel |= low;
-      fifo ^= low;
-    }
-    fifo = sel;
-  }
-  return (uint32_t)(((fifo << head) | (fifo >> (S - head))) & full);
-}
-
-__device__ inline uint32_t lane_id() { return __lane_id(); }
-
-// Inclusive prefix sum over the 64 lanes of a wave (all lanes must be active).
-__device__ inline uint32_t wave_incl_scan(uint32_t x) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, off);
-    if (lane >= (uint32_t)off) x += y;
-  }
-  return x;
-}
 
 // Expands one frontier node u of slot o at level d (Cluster::run_gossip body,
 // gossip.rs:511-609), in three phases so that no memory round trip waits on
@@ -602,15 +539,6 @@ struct CpArgs {
   size_t PAIRS;
 };
 
-// u64 -> f64 -> u64 of received_cache.rs:114, saturating like Rust's `as u64`.
-__device__ inline uint64_t min_ingress_stake(uint64_t stake, double thr) {
-  const double x = (double)stake * thr;
-  if (!(x > 0.0)) return 0;
-  if (x >= 18446744073709551616.0) return ~0ull;
-  return (uint64_t)x;
-}
-
-__device__ inline uint64_t sat_add(uint64_t a, uint64_t b) { return a + b < a ? ~0ull : a + b; }
 
 // prune_connections -> PushActiveSet::prune(prunee u, pruner v, [origin]) for one
 // prunee (gossip.rs:701-737, push_active_set.rs:56-71,143-151): set the prune bit
@@ -630,36 +558,6 @@ __device__ inline void apply_prune(const CpArgs& a, uint32_t o, uint32_t ob, uin
       return;
     }
   }
-}
-
-// Maximum of x (< 32) over the wave's ACTIVE lanes, wave-uniform. Built from
-// ballots, which see exactly the active lanes; a shuffle butterfly would read
-// stale registers of lanes switched off by an enclosing divergent branch.
-__device__ inline uint32_t active_max_small(uint32_t x) {
-  uint32_t m = 0;
-#pragma unroll
-  for (uint32_t b = 16; b; b >>= 1)
-    if (__ballot(x >= m + b)) m += b;
-  return __builtin_amdgcn_readfirstlane(m);
-}
-
-__device__ inline void cswap(uint32_t& x, uint32_t& y) {
-  const uint32_t lo = min(x, y), hi = max(x, y);
-  x = lo;
-  y = hi;
-}
-
-// Batcher odd-even merge sort of 16 keys (63 comparators), register-resident.
-__device__ inline void sort16(uint32_t (&r)[16]) {
-#pragma unroll
-  for (int p = 1; p < 16; p <<= 1)
-#pragma unroll
-    for (int k = p; k >= 1; k >>= 1)
-#pragma unroll
-      for (int j = k % p; j + k < 16; j += 2 * k)
-#pragma unroll
-        for (int i = 0; i < k; ++i)
-          if (i + j + k < 16 && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cswap(r[i + j], r[i + j + k]);
 }
 
 // Generic per-pair path (any in-degree / cache length): state read and written in place.

@@ -1,0 +1,773 @@
+// gs_round_wg.hip -- one whole gossip round of one origin slot inside one workgroup.
+//
+// The per-slot state of a round fits in LDS for clusters up to a few thousand
+// nodes (C2: 3,000 nodes -> ~80 KB), so a single kernel runs, per slot:
+//   A  Cluster::run_gossip BFS (gossip.rs:494-615): frontier queues, in-degree
+//      counters, hop table and each node's push mask in LDS;
+//   B  the inbound lists ("orders", gossip.rs:601-607) as an LDS CSR: segment
+//      offsets from a wave-aggregated scan of the in-degrees, then every visited
+//      node scatters its id into its peers' segments -- the records never touch
+//      HBM; per-pair hops/in-degree/egress and the measured-round statistics are
+//      written in the same pass;
+//   C  consume_messages + ReceivedCache::record (gossip.rs:618-653,
+//      received_cache.rs:27-36,83-98): per receiving node, its records sorted by
+//      (hop, id) in registers, looked up in the node's cache entry (HBM,
+//      slot-major rows, coalesced across lanes);
+//   D  send_prunes + ReceivedCache::prune + prune_connections (gossip.rs:657-737,
+//      received_cache.rs:38-63,100-131) for the entries that reached 20 upserts:
+//      (score, stake) order as one 31-bit key ((127 - score) << 24 | stake rank)
+//      sorted in registers, pre-add cumulative stake, prune bits set in the
+//      prunees' masks;
+//   E  the round summary (gossip_main.rs:480-514): hop histogram, stranded
+//      count/stake order statistics from an LDS bitmap over stake rank.
+// In-degree > 16 or cache entries > 32 keys take a wave-cooperative path
+// (one wave per node) so a few heavy nodes do not serialize their wave.
+#include <type_traits>
+
+#include "gs_device.h"
+#include "gs_internal.h"
+
+namespace gs {
+
+constexpr uint32_t RWG_THREADS = 512;
+constexpr uint32_t RWG_WAVES = RWG_THREADS / 64;
+constexpr uint32_t RWG_SCR = 128;  // per-wave LDS scratch (u32): staged cache keys / prune keys
+constexpr uint32_t LANE_C = 16;    // register path: in-degree <= 16
+constexpr uint32_t LANE_L = 32;    // register prune path: cache entry <= 32 keys
+
+struct RoundArgs {
+  const uint64_t* stake;
+  const uint8_t* bucket;
+  const uint32_t* peers;
+  const uint16_t* hl;
+  const uint32_t* frank;
+  const uint32_t* srank;
+  const uint32_t* by_srank;
+  const uint32_t* prank;     // rank by (stake desc, id asc): the prune order's tie-broken stake key
+  const uint32_t* by_prank;
+  const uint64_t* pstake;    // stake by prune rank
+  const uint32_t* origin;
+  const uint8_t* obkt;
+  const uint32_t* nfail;
+  const uint32_t* min_ingress;
+  const double* thr;
+  uint32_t* slot_prunes;
+  uint8_t* hops;
+  uint32_t* cnt;
+  uint32_t* mask;
+  uint32_t* cmeta;
+  uint32_t* ckey;
+  uint8_t* cscore;
+  uint8_t* egress;
+  uint8_t* prune_round;
+  uint32_t* egress_acc;
+  uint32_t* ingress_acc;
+  uint32_t* prune_acc;
+  uint32_t* strand;
+  uint64_t* hist_acc;
+  gs_round_summary* sum;  // this round's row [S] of the summary ring (record only)
+  uint32_t* err;
+  unsigned long long* phase_clk;  // optional: per-phase clock sums (thread 0 of each workgroup)
+  uint32_t wave_c_max;            // in-degree bound of the wave consume path (64; 24 for path coverage)
+  uint32_t N, S, ASZ, fanout, fcap;
+  size_t PAIRS;
+  int record;
+};
+
+// Phase clock: thread 0 adds the time since the last mark to phase_clk[ph].
+#define RWG_MARK(ph)                                                              \
+  do {                                                                            \
+    if (a.phase_clk && tid == 0) {                                                \
+      const unsigned long long now_ = wall_clock64();                             \
+      atomicAdd(&a.phase_clk[ph], now_ - t_mark);                                 \
+      t_mark = now_;                                                              \
+    }                                                                             \
+  } while (0)
+
+// LDS carve-up (byte offsets), shared by the host's size query and the kernel.
+struct RwgLayout {
+  uint32_t ctrl, hist, scr, cnt, qo, pm, nl, hops, bm, rec, total;
+};
+// pmw: bytes per push mask (2 when the ring has <= 16 slots)
+__host__ __device__ inline RwgLayout rwg_layout(uint32_t N, uint32_t fcap, uint32_t pmw) {
+  RwgLayout L;
+  uint32_t o = 0;
+  L.ctrl = o; o += 32 * 4;
+  L.hist = o; o += 256 * 4;
+  L.scr = o;  o += RWG_WAVES * RWG_SCR * 4;
+  L.cnt = o;  o += 4 * N;                       // in-degree (u32 atomics)
+  L.qo = o;   o += 4 * N;                       // BFS queues 2 x u16[N], then segment ends u32[N]
+  L.pm = o;   o += (pmw * N + 3) & ~3u;         // push masks, then the heavy-node list u16[N]
+  L.nl = o;   o += (2 * N + 3) & ~3u;           // per node: ring head | len << 5 | entry bucket << 11
+  L.hops = o; o += (N + 3) & ~3u;
+  L.bm = o;   o += ((N + 31) / 32) * 4;         // stranded bitmap over stake rank
+  L.rec = o;  o += (2 * fcap * N + 3) & ~3u;    // inbound sources u16, CSR by destination
+  L.total = o;
+  return L;
+}
+
+size_t round_wg_lds_bytes(uint32_t N, uint32_t fcap, uint32_t ASZP) {
+  return rwg_layout(N, fcap, ASZP <= 16 ? 2 : 4).total;
+}
+
+// ctrl words
+enum { C_QN = 0, C_NEXT = 1, C_ERR = 2, C_SEG = 3, C_VIS = 4, C_PUSH = 5, C_STR = 6, C_PRUNES = 7, C_SSUM = 8,
+       C_NHC = 10, C_NHP = 11, C_KTH = 12, C_HCNT = 16, C_HSUM = 18, C_HMIN = 20, C_HMAX = 21, C_HMLO = 22,
+       C_HMHI = 23 };
+
+__device__ inline void apply_prune_r(const RoundArgs& a, size_t base, const uint16_t* nl_l, uint32_t u, uint32_t v) {
+  // PushActiveSet::prune for one (prunee u, pruner v) pair (push_active_set.rs:56-71,143-151)
+  const uint32_t nl = nl_l[u];
+  const uint32_t ent = u * NB + (nl >> 11);
+  const uint32_t head = nl & 31u, L = (nl >> 5) & 63u;
+  const uint32_t* row = a.peers + (size_t)ent * ((a.ASZ + 3) & ~3u);
+  for (uint32_t j = 0; j < L; ++j) {
+    uint32_t slot = head + j;
+    if (slot >= a.ASZ) slot -= a.ASZ;
+    if (row[slot] == v) {
+      atomicOr(&a.mask[base + u], 1u << slot);
+      return;
+    }
+  }
+}
+
+// ---- C: register path (1 <= c <= 16) ----
+__device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t* recs, const uint8_t* hops_l,
+                                    uint32_t c, uint32_t& len, uint32_t& up, uint32_t& errf) {
+  const size_t PAIRS = a.PAIRS;
+  const uint32_t q = (uint32_t)p;
+  uint32_t rk[16];
+  const uint32_t wc = active_max<5>(c);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    rk[j] = 0xFFFFFFFFu;
+    if ((uint32_t)j < wc) {
+      const uint32_t s = recs[min((uint32_t)j, c - 1)];
+      const uint32_t key = ((uint32_t)hops_l[s] << 16) | s;  // (hop, id): hop = dist[src] + 1 shifts all alike
+      rk[j] = (uint32_t)j < c ? key : 0xFFFFFFFFu;
+    }
+  }
+  sort_net<16>(rk);
+  // look the records up in the entry: rows streamed 8 at a time, loads issued together
+  uint32_t present = 0;
+  int idx0 = -1, idx1 = -1;
+  const uint32_t wl = active_max<7>(len);
+  for (uint32_t i0 = 0; i0 < wl; i0 += 8) {
+    uint32_t kc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) kc[t] = i0 + t < wl ? (a.ckey + (size_t)(i0 + t) * PAIRS)[q] : 0xFFFFFFFEu;
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const uint32_t i = i0 + t;
+      const uint32_t k = i < len ? kc[t] : 0xFFFFFFFEu;
+      uint32_t m = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) m |= (uint32_t)((rk[j] & 0xFFFFu) == k) << j;
+      present |= m;
+      if (m & 1u) idx0 = (int)i;
+      if (m & 2u) idx1 = (int)i;
+    }
+  }
+  up = up < 255 ? up + 1 : 255;  // rank 0 (received_cache.rs:84-86)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {  // timely: score += 1, inserted regardless of the 50-key cap
+    if ((uint32_t)j >= c) break;
+    const int idx = j == 0 ? idx0 : idx1;
+    if (idx >= 0) {
+      uint8_t* sp = a.cscore + (size_t)idx * PAIRS + p;
+      const uint32_t s0 = *sp & 0x7Fu;
+      *sp = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
+    } else if (len < CACHE_CAP) {
+      (a.ckey + (size_t)len * PAIRS)[q] = rk[j] & 0xFFFFu;
+      (a.cscore + (size_t)len * PAIRS)[q] = 1;
+      ++len;
+    } else {
+      errf |= ERR_CACHE;
+    }
+  }
+#pragma unroll
+  for (int j = 2; j < 16; ++j) {  // rank order; inserted only while len < 50 (received_cache.rs:91-97)
+    if ((uint32_t)j < c && !((present >> j) & 1u) && len < CACHE_LIMIT) {
+      (a.ckey + (size_t)len * PAIRS)[q] = rk[j] & 0xFFFFu;
+      (a.cscore + (size_t)len * PAIRS)[q] = 0;
+      ++len;
+    }
+  }
+}
+
+// ---- D: register path (len <= 32). Rows are rewritten in prune order with the
+// pruned flag; returns the number of prunees. ----
+__device__ inline uint32_t prune_lane(const RoundArgs& a, size_t base, const uint16_t* nl_l, uint32_t org, size_t p,
+                                      uint32_t v, uint32_t len, uint32_t mi, uint64_t mis) {
+  const size_t PAIRS = a.PAIRS;
+  const uint32_t q = (uint32_t)p;
+  const uint32_t wl = active_max<6>(len);
+  uint32_t sk[32];
+  {
+    uint32_t kk[32], ss[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      kk[i] = 0;
+      ss[i] = 0;
+      if ((uint32_t)i < wl) {
+        kk[i] = (a.ckey + (size_t)i * PAIRS)[q];
+        ss[i] = (a.cscore + (size_t)i * PAIRS)[q];
+      }
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const bool in = (uint32_t)i < len;
+      const uint32_t pr = a.prank[in ? kk[i] : 0u];
+      sk[i] = in ? (((0x7Fu - (ss[i] & 0x7Fu)) << 24) | pr) : 0xFFFFFFFFu;
+    }
+  }
+  if (wl <= 16) sort_net<16>(sk);
+  else sort_net<32>(sk);
+  // sorted_unstable_by_key(Reverse((score, stake))), ties by id; scan of pre-add
+  // cumulative stake; skip(min_ingress_nodes); skip_while(cum < min_ingress_stake)
+  uint64_t cum = 0;
+  uint32_t first = len, npr = 0;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    if ((uint32_t)i < len) {
+      const uint32_t pr = sk[i] & 0xFFFFFFu;
+      const uint32_t node = a.by_prank[pr];
+      const uint64_t st = a.pstake[pr];
+      const bool tail = (uint32_t)i >= mi && cum >= mis;
+      if (tail && first == len) first = (uint32_t)i;
+      const bool pruned = tail && node != org;
+      npr += pruned;
+      (a.ckey + (size_t)i * PAIRS)[q] = node;
+      (a.cscore + (size_t)i * PAIRS)[q] = (uint8_t)((0x7Fu - (sk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
+      cum = sat_add(cum, st);
+    }
+  }
+  for (uint32_t i = first; i < len; ++i) {  // prune_connections
+    const uint32_t u = (a.ckey + (size_t)i * PAIRS)[q];
+    if (u != org) apply_prune_r(a, base, nl_l, u, v);
+  }
+  return npr;
+}
+
+// ---- C: wave path (16 < c <= 64), all 64 lanes on one node; len/up uniform ----
+__device__ inline void consume_wave(const RoundArgs& a, size_t p, const uint16_t* recs, const uint8_t* hops_l,
+                                    uint32_t c, uint32_t& len, uint32_t& up, uint32_t* scr, uint32_t& errf) {
+  const size_t PAIRS = a.PAIRS;
+  const uint32_t q = (uint32_t)p;
+  const uint32_t l = lane_id();
+  uint32_t key = 0xFFFFFFFFu;
+  if (l < c) {
+    const uint32_t s = recs[l];
+    key = ((uint32_t)hops_l[s] << 16) | s;
+  }
+#pragma unroll
+  for (uint32_t k = 2; k <= 64; k <<= 1)  // bitonic sort across the wave, ascending by lane
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t other = (uint32_t)__shfl_xor((int)key, (int)j);
+      const bool asc = (l & k) == 0;
+      const bool lower = (l & j) == 0;
+      key = (lower == asc) ? min(key, other) : max(key, other);
+    }
+  const uint32_t src = key & 0xFFFFu;
+  const uint32_t L0 = len;
+  for (uint32_t i = l; i < L0; i += 64) scr[i] = (a.ckey + (size_t)i * PAIRS)[q];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  int found = -1;
+  if (l < c)
+    for (uint32_t i = 0; i < L0; ++i)
+      if (scr[i] == src) found = (int)i;
+  const bool isnew = l < c && found < 0;
+  const uint64_t nb = __ballot(isnew);
+  const uint32_t n0 = (uint32_t)(nb & 1u), n1 = (uint32_t)((nb >> 1) & 1u);
+  up = up < 255 ? up + 1 : 255;
+  if (l < 2) {
+    if (found >= 0) {
+      uint8_t* sp = a.cscore + (size_t)found * PAIRS + p;
+      const uint32_t s0 = *sp & 0x7Fu;
+      *sp = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
+    } else {
+      const uint32_t pos = L0 + (l == 1 ? n0 : 0u);
+      if (pos < CACHE_CAP) {
+        (a.ckey + (size_t)pos * PAIRS)[q] = src;
+        (a.cscore + (size_t)pos * PAIRS)[q] = 1;
+      } else {
+        errf |= ERR_CACHE;
+      }
+    }
+  }
+  const uint32_t L1 = min(L0 + n0 + n1, CACHE_CAP);
+  const uint64_t rest = nb & ~3ull;
+  if (l >= 2 && isnew) {
+    const uint32_t pos = L1 + (uint32_t)__popcll(rest & ((1ull << l) - 1));
+    if (pos < CACHE_LIMIT) {
+      (a.ckey + (size_t)pos * PAIRS)[q] = src;
+      (a.cscore + (size_t)pos * PAIRS)[q] = 0;
+    }
+  }
+  const uint32_t nrest = (uint32_t)__popcll(rest);
+  len = L1 + (L1 < CACHE_LIMIT ? min(nrest, CACHE_LIMIT - L1) : 0u);
+}
+
+// ---- C: any in-degree (c > 64): lane 0 of the wave, records selected in order ----
+__device__ inline void consume_serial(const RoundArgs& a, size_t p, const uint16_t* recs, const uint8_t* hops_l,
+                                      uint32_t c, uint32_t& len, uint32_t& up, uint32_t& errf) {
+  const size_t PAIRS = a.PAIRS;
+  const uint32_t l = lane_id();
+  uint32_t ln = len, u = up;
+  if (l == 0) {
+    uint32_t prev = 0;
+    u = u < 255 ? u + 1 : 255;
+    for (uint32_t k = 0; k < c; ++k) {
+      uint32_t best = 0xFFFFFFFFu;
+      for (uint32_t j = 0; j < c; ++j) {
+        const uint32_t s = recs[j];
+        const uint32_t key = ((uint32_t)hops_l[s] << 16) | s;
+        if ((k == 0 || key > prev) && key < best) best = key;
+      }
+      prev = best;
+      const uint32_t src = best & 0xFFFFu;
+      int found = -1;
+      for (uint32_t i = 0; i < ln; ++i)
+        if (a.ckey[(size_t)i * PAIRS + p] == src) { found = (int)i; break; }
+      if (k < 2) {
+        if (found >= 0) {
+          uint8_t* sp = a.cscore + (size_t)found * PAIRS + p;
+          const uint32_t s0 = *sp & 0x7Fu;
+          *sp = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
+        } else if (ln < CACHE_CAP) {
+          a.ckey[(size_t)ln * PAIRS + p] = src;
+          a.cscore[(size_t)ln * PAIRS + p] = 1;
+          ++ln;
+        } else {
+          errf |= ERR_CACHE;
+        }
+      } else if (found < 0 && ln < CACHE_LIMIT) {
+        a.ckey[(size_t)ln * PAIRS + p] = src;
+        a.cscore[(size_t)ln * PAIRS + p] = 0;
+        ++ln;
+      }
+    }
+  }
+  len = (uint32_t)__shfl((int)ln, 0);
+  up = (uint32_t)__shfl((int)u, 0);
+}
+
+// ---- D: wave path (any len <= 96), two entries per lane ----
+__device__ inline uint32_t prune_wave(const RoundArgs& a, size_t base, const uint16_t* nl_l, uint32_t org, size_t p,
+                                      uint32_t v, uint32_t len, uint32_t mi, uint64_t mis, uint32_t* scr) {
+  const size_t PAIRS = a.PAIRS;
+  const uint32_t q = (uint32_t)p;
+  const uint32_t l = lane_id();
+  __threadfence_block();  // this wave's consume writes to the entry's rows
+  uint32_t sk[2], nd[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t i = l + 64 * t;
+    sk[t] = 0xFFFFFFFFu;
+    nd[t] = 0;
+    if (i < len) {
+      nd[t] = (a.ckey + (size_t)i * PAIRS)[q];
+      const uint32_t sc = (a.cscore + (size_t)i * PAIRS)[q] & 0x7Fu;
+      sk[t] = ((0x7Fu - sc) << 24) | a.prank[nd[t]];
+    }
+    scr[i] = sk[t];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  uint32_t rank[2] = {0, 0};
+  uint64_t cum[2] = {0, 0};
+  for (uint32_t j = 0; j < len; ++j) {
+    const uint32_t x = scr[j];
+    const uint64_t st = a.pstake[x & 0xFFFFFFu];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      if (x < sk[t]) { ++rank[t]; cum[t] = sat_add(cum[t], st); }  // saturating sums are order-free
+  }
+  uint32_t npr = 0;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t i = l + 64 * t;
+    bool pruned = false;
+    if (i < len) {
+      pruned = rank[t] >= mi && cum[t] >= mis && nd[t] != org;
+      (a.ckey + (size_t)rank[t] * PAIRS)[q] = nd[t];
+      (a.cscore + (size_t)rank[t] * PAIRS)[q] = (uint8_t)((0x7Fu - (sk[t] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
+      if (pruned) apply_prune_r(a, base, nl_l, nd[t], v);
+    }
+    npr += (uint32_t)__popcll(__ballot(pruned));
+  }
+  return npr;
+}
+
+// Finishes a node's cache step: prune when due (lane path), else clear the
+// previous round's pruned-len and record no prunes.
+__device__ inline void finish_node(const RoundArgs& a, size_t p, uint32_t meta, uint32_t len, uint32_t up,
+                                   uint32_t npr_if_pruned, bool pruned_now) {
+  uint32_t nm;
+  if (pruned_now) nm = len << 16;  // std::mem::take: entry reset, pruned keys kept readable
+  else nm = len | (up << 8);
+  if (nm != meta) a.cmeta[p] = nm;
+  const uint32_t npr = pruned_now ? npr_if_pruned : 0u;
+  a.prune_round[p] = (uint8_t)(npr < 255 ? npr : 255);
+  if (a.record && npr) a.prune_acc[p] += npr;
+}
+
+// Wave 0 finds up to four order statistics (0-based ranks ks[]) of the set bits of
+// an LDS bitmap of W words; results in out[].
+__device__ inline void wave_kth_bits(const uint32_t* bm, uint32_t W, const uint32_t (&ks)[4], uint32_t* out) {
+  const uint32_t l = lane_id();
+  const uint32_t chunk = (W + 63) / 64;
+  const uint32_t lo = min(W, l * chunk), hi = min(W, lo + chunk);
+  uint32_t pc = 0;
+  for (uint32_t i = lo; i < hi; ++i) pc += __popc(bm[i]);
+  const uint32_t incl = wave_incl_scan(pc);
+  const uint32_t before = incl - pc;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t k = ks[t];
+    if (k >= before && k < incl) {
+      uint32_t need = k - before;
+      for (uint32_t i = lo; i < hi; ++i) {
+        uint32_t w = bm[i];
+        const uint32_t c = __popc(w);
+        if (need < c) {
+          for (uint32_t j = 0; j < need; ++j) w &= w - 1;
+          out[t] = i * 32 + (__ffs(w) - 1);
+          break;
+        }
+        need -= c;
+      }
+    }
+  }
+}
+
+// Wave 0: HopsStat inputs from the round's hop histogram (bins 1..254 = reached
+// non-origin nodes): count, sum, min, max and the two median bins.
+__device__ inline void wave_hop_stats(const uint32_t* hist, uint32_t* ctrl) {
+  const uint32_t l = lane_id();
+  uint32_t h[4], c = 0;
+  uint64_t s = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t i = 4 * l + t;
+    h[t] = (i >= 1 && i < 255) ? hist[i] : 0u;
+    c += h[t];
+    s += (uint64_t)i * h[t];
+  }
+  const uint32_t incl = wave_incl_scan(c);
+  const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+  const uint32_t before = incl - c;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)s, off);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(s >> 32), off);
+    s += ((uint64_t)hi << 32) | lo;
+  }
+  const uint64_t nz = __ballot(c > 0);
+  if (l == 0) {
+    ctrl[C_HCNT] = total;
+    *reinterpret_cast<unsigned long long*>(&ctrl[C_HSUM]) = s;
+  }
+  if (!total) return;
+  if (l == (uint32_t)(__ffsll((long long)nz) - 1)) {
+    for (int t = 0; t < 4; ++t)
+      if (h[t]) { ctrl[C_HMIN] = 4 * l + t; break; }
+  }
+  if (l == 63u - (uint32_t)__clzll((long long)nz)) {
+    for (int t = 3; t >= 0; --t)
+      if (h[t]) { ctrl[C_HMAX] = 4 * l + t; break; }
+  }
+  const uint32_t ks[2] = {total % 2 ? total / 2 : total / 2 - 1, total / 2};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (ks[q] >= before && ks[q] < incl) {
+      uint32_t run = before;
+      for (int t = 0; t < 4; ++t) {
+        if (ks[q] < run + h[t]) { ctrl[C_HMLO + q] = 4 * l + t; break; }
+        run += h[t];
+      }
+    }
+  }
+}
+
+template <int ASZP>
+__global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
+  using PMT = typename std::conditional<(ASZP <= 16), uint16_t, uint32_t>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t N = a.N;
+  const RwgLayout L = rwg_layout(N, a.fcap, (uint32_t)sizeof(PMT));
+  uint32_t* ctrl = reinterpret_cast<uint32_t*>(smem + L.ctrl);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + L.hist);
+  uint32_t* cnt_l = reinterpret_cast<uint32_t*>(smem + L.cnt);
+  uint16_t* q0 = reinterpret_cast<uint16_t*>(smem + L.qo);
+  uint16_t* q1 = q0 + N;
+  uint32_t* off_l = reinterpret_cast<uint32_t*>(smem + L.qo);
+  PMT* pm_l = reinterpret_cast<PMT*>(smem + L.pm);
+  uint16_t* hv_l = reinterpret_cast<uint16_t*>(smem + L.pm);  // heavy nodes: consume from the front,
+                                                              // prune-only from the back
+  uint16_t* nl_l = reinterpret_cast<uint16_t*>(smem + L.nl);
+  uint8_t* hops_l = smem + L.hops;
+  uint32_t* bm_l = reinterpret_cast<uint32_t*>(smem + L.bm);
+  uint16_t* rec_l = reinterpret_cast<uint16_t*>(smem + L.rec);
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint32_t* scr = reinterpret_cast<uint32_t*>(smem + L.scr) + wid * RWG_SCR;
+  const uint32_t W = (N + 31) / 32;
+
+  const uint32_t o = blockIdx.x;
+  const uint32_t org = a.origin[o], ob = a.obkt[o], nf = a.nfail[o];
+  const size_t base = (size_t)o * N;
+  uint32_t errf = 0;
+  unsigned long long t_mark = a.phase_clk && tid == 0 ? wall_clock64() : 0;
+
+  for (uint32_t v = tid; v < N; v += RWG_THREADS) {
+    cnt_l[v] = 0;
+    hops_l[v] = 0xFF;
+    pm_l[v] = 0;
+    const uint32_t b = min((uint32_t)a.bucket[v], ob);  // entry the origin uses (push_active_set.rs:38-52)
+    const uint32_t hv = a.hl[v * NB + b];
+    nl_l[v] = (uint16_t)((hv & 0x1Fu) | ((hv >> 8) << 5) | (b << 11));
+  }
+  for (uint32_t i = tid; i < 256; i += RWG_THREADS) hist[i] = 0;
+  for (uint32_t i = tid; i < W; i += RWG_THREADS) bm_l[i] = 0;
+  if (tid < 32) ctrl[tid] = 0;
+  __syncthreads();
+  if (tid == 0) { ctrl[C_QN] = 1; hops_l[org] = 0; q0[0] = (uint16_t)org; }
+  __syncthreads();
+  RWG_MARK(0);
+
+  // ---------------- A: BFS -------------------------------------------------
+  uint16_t* cur = q0;
+  uint16_t* nxt = q1;
+  for (uint32_t d = 0;; ++d) {
+    const uint32_t qn = ctrl[C_QN];
+    if (qn == 0) break;
+    if (d + 1 >= 255) { errf |= ERR_DEPTH; break; }
+    for (uint32_t i0 = 0; i0 < qn; i0 += RWG_THREADS) {
+      const bool valid = i0 + tid < qn;
+      uint32_t row[ASZP];
+      uint32_t pushm = 0;
+      if (valid) {
+        const uint32_t u = cur[i0 + tid];
+        const uint32_t pmask = a.mask[base + u];
+        const uint32_t nl = nl_l[u];
+        load_row<ASZP>(a.peers + (size_t)(u * NB + (nl >> 11)) * ASZP, row);
+        pushm = taken_slots<ASZP>(row, nl & 31u, (nl >> 5) & 63u, a.ASZ, pmask, org, a.fanout);
+        if (nf) {  // failed peers burn their fanout slot (gossip.rs:538-541)
+#pragma unroll
+          for (int s = 0; s < ASZP; ++s)
+            if (((pushm >> s) & 1u) && a.frank[row[s]] < nf) pushm &= ~(1u << s);
+        }
+        pm_l[u] = (PMT)pushm;
+      } else {
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s) row[s] = 0;
+      }
+      uint32_t old[ASZP];
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) old[s] = ((pushm >> s) & 1u) ? atomicAdd(&cnt_l[row[s]], 1u) : 1u;
+      uint32_t newm = 0;
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s)
+        if (((pushm >> s) & 1u) && old[s] == 0) {
+          newm |= 1u << s;
+          hops_l[row[s]] = (uint8_t)(d + 1);
+        }
+      const uint32_t k = __popc(newm);
+      uint32_t idx = k ? atomicAdd(&ctrl[C_NEXT], k) : 0;
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s)
+        if ((newm >> s) & 1u) nxt[idx++] = (uint16_t)row[s];
+    }
+    __syncthreads();
+    if (tid == 0) { ctrl[C_QN] = ctrl[C_NEXT]; ctrl[C_NEXT] = 0; }
+    uint16_t* t = cur; cur = nxt; nxt = t;
+    __syncthreads();
+  }
+
+  RWG_MARK(1);
+  // ---------------- B: inbound CSR, per-pair outputs, round statistics ------
+  for (uint32_t v0 = 0; v0 < N; v0 += RWG_THREADS) {  // segment per destination (order free)
+    const uint32_t v = v0 + tid;
+    const uint32_t c = v < N ? cnt_l[v] : 0;
+    const uint32_t incl = wave_incl_scan(c);
+    const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+    uint32_t b = 0;
+    if (lane == 0 && tot) b = atomicAdd(&ctrl[C_SEG], tot);
+    b = (uint32_t)__shfl((int)b, 0);
+    if (v < N) off_l[v] = b + incl - c;
+  }
+  __syncthreads();
+  {
+    uint32_t vis = 0, pushes = 0, sc = 0;
+    uint64_t ss = 0;
+    for (uint32_t v = tid; v < N; v += RWG_THREADS) {
+      const size_t p = base + v;
+      const uint32_t h = hops_l[v], c = cnt_l[v];
+      const uint32_t pmv = h != 0xFF ? pm_l[v] : 0u;
+      const uint32_t eg = __popc(pmv);
+      a.hops[p] = (uint8_t)h;
+      a.cnt[p] = c;
+      a.egress[p] = (uint8_t)eg;
+      if (a.record) {  // measured-round statistics (gossip_main.rs:480-514)
+        pushes += c;
+        if (c) a.ingress_acc[p] += c;
+        if (eg) a.egress_acc[p] += eg;
+        if (h != 0xFF) {
+          ++vis;
+          atomicAdd(&hist[h], 1u);
+        } else if (!(nf && a.frank[v] < nf)) {
+          a.strand[p] += 1;
+          ++sc;
+          ss += a.stake[v];
+          const uint32_t r = a.srank[v];
+          atomicOr(&bm_l[r >> 5], 1u << (r & 31));
+        }
+      }
+      if (pmv) {
+        uint32_t row[ASZP];
+        load_row<ASZP>(a.peers + (size_t)(v * NB + (nl_l[v] >> 11)) * ASZP, row);
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s)
+          if ((pmv >> s) & 1u) rec_l[atomicAdd(&off_l[row[s]], 1u)] = (uint16_t)v;
+      }
+    }
+    if (a.record) {
+      if (vis) atomicAdd(&ctrl[C_VIS], vis);
+      if (pushes) atomicAdd(&ctrl[C_PUSH], pushes);
+      if (sc) atomicAdd(&ctrl[C_STR], sc);
+      if (ss) atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[C_SSUM]), (unsigned long long)ss);
+    }
+  }
+  __syncthreads();
+  RWG_MARK(2);
+
+  // ---------------- C + D: consume, prune (register path) -------------------
+  const uint32_t mi = a.min_ingress[o];
+  const double thr = a.thr[o];
+  const uint64_t so = a.stake[org];
+  uint32_t npr_sum = 0;
+  for (uint32_t v = tid; v < N; v += RWG_THREADS) {
+    const size_t p = base + v;
+    const uint32_t c = cnt_l[v];
+    if (c > LANE_C) {
+      hv_l[atomicAdd(&ctrl[C_NHC], 1u)] = (uint16_t)v;
+      continue;
+    }
+    const uint32_t meta = a.cmeta[p];
+    uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
+    if (c) consume_lane(a, p, rec_l + (off_l[v] - c), hops_l, c, len, up, errf);
+    if (up >= MIN_NUM_UPSERTS) {
+      if (len > LANE_L) {
+        a.cmeta[p] = len | (up << 8);
+        hv_l[N - 1 - atomicAdd(&ctrl[C_NHP], 1u)] = (uint16_t)v;
+        continue;
+      }
+      const uint64_t sv = a.stake[v];
+      const uint32_t npr = prune_lane(a, base, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr));
+      npr_sum += npr;
+      finish_node(a, p, meta, len, 0, npr, true);
+    } else {
+      finish_node(a, p, meta, len, up, 0, false);
+    }
+  }
+  __syncthreads();
+  RWG_MARK(3);
+
+  // ---------------- C + D: heavy nodes, one wave each -----------------------
+  {
+    const uint32_t nhc = ctrl[C_NHC], nhp = ctrl[C_NHP];
+    for (uint32_t i = wid; i < nhc + nhp; i += RWG_WAVES) {
+      const bool is_c = i < nhc;
+      const uint32_t v = is_c ? hv_l[i] : hv_l[N - 1 - (i - nhc)];
+      const size_t p = base + v;
+      const uint32_t meta = a.cmeta[p];
+      uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
+      if (is_c) {
+        const uint32_t c = cnt_l[v];
+        const uint16_t* recs = rec_l + (off_l[v] - c);
+        if (c <= a.wave_c_max) consume_wave(a, p, recs, hops_l, c, len, up, scr, errf);
+        else consume_serial(a, p, recs, hops_l, c, len, up, errf);
+      }
+      const bool due = up >= MIN_NUM_UPSERTS;
+      uint32_t npr = 0;
+      if (due) {
+        const uint64_t sv = a.stake[v];
+        npr = prune_wave(a, base, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr), scr);
+        if (lane == 0) npr_sum += npr;
+      }
+      if (lane == 0) finish_node(a, p, meta, len, due ? 0u : up, npr, due);
+    }
+  }
+  if (npr_sum) atomicAdd(&ctrl[C_PRUNES], npr_sum);
+  if (errf) atomicOr(&ctrl[C_ERR], errf);
+  __syncthreads();
+  RWG_MARK(4);
+
+  // ---------------- E: slot summary -----------------------------------------
+  if (tid == 0) {
+    a.slot_prunes[o] = ctrl[C_PRUNES];
+    if (ctrl[C_ERR]) atomicOr(a.err, ctrl[C_ERR]);
+  }
+  if (!a.record) return;
+  for (uint32_t i = tid; i < 256; i += RWG_THREADS)
+    if (hist[i]) a.hist_acc[(size_t)o * 256 + i] += hist[i];
+  const uint32_t sc = ctrl[C_STR];
+  if (wid == 0) wave_hop_stats(hist, ctrl);
+  if (wid == 1 && sc) {
+    const uint32_t ks[4] = {0u, sc - 1, sc % 2 ? sc / 2 : sc / 2 - 1, sc / 2};
+    wave_kth_bits(bm_l, W, ks, &ctrl[C_KTH]);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    gs_round_summary s = {};
+    s.visited = ctrl[C_VIS];
+    s.pushes = ctrl[C_PUSH];
+    s.stranded = sc;
+    s.prunes = ctrl[C_PRUNES];
+    s.stranded_stake_sum = *reinterpret_cast<unsigned long long*>(&ctrl[C_SSUM]);
+    s.hop_count = ctrl[C_HCNT];  // HopsStat over reached non-origin nodes (gossip_stats.rs:47-98)
+    s.hop_sum = *reinterpret_cast<unsigned long long*>(&ctrl[C_HSUM]);
+    if (s.hop_count) {
+      s.hop_min = ctrl[C_HMIN];
+      s.hop_max = ctrl[C_HMAX];
+      s.hop_med_lo = ctrl[C_HMLO];
+      s.hop_med_hi = ctrl[C_HMHI];
+    }
+    if (sc) {  // StrandedNodeStats order statistics by stake (gossip_stats.rs:767-819)
+      s.stranded_stake_min = a.stake[a.by_srank[ctrl[C_KTH + 0]]];
+      s.stranded_stake_max = a.stake[a.by_srank[ctrl[C_KTH + 1]]];
+      s.stranded_med_lo = a.stake[a.by_srank[ctrl[C_KTH + 2]]];
+      s.stranded_med_hi = a.stake[a.by_srank[ctrl[C_KTH + 3]]];
+    }
+    a.sum[o] = s;
+  }
+  RWG_MARK(5);
+}
+
+hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_slot) {
+  RoundArgs a;
+  a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.frank = e.frank; a.srank = e.srank;
+  a.by_srank = e.by_srank; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake; a.origin = e.origin;
+  a.obkt = e.obkt; a.nfail = e.nfail; a.min_ingress = e.min_ingress; a.thr = e.thr; a.slot_prunes = e.slot_prunes;
+  a.hops = e.hops; a.cnt = e.cnt; a.mask = e.mask; a.cmeta = e.cmeta; a.ckey = e.ckey; a.cscore = e.cscore;
+  a.egress = e.egress; a.prune_round = e.prune_round; a.egress_acc = e.egress_acc; a.ingress_acc = e.ingress_acc;
+  a.prune_acc = e.prune_acc; a.strand = e.strand; a.hist_acc = e.hist_acc;
+  a.sum = record ? e.sum + (size_t)rec_slot * e.S : nullptr;
+  a.err = e.err; a.phase_clk = e.phase_clk;
+  a.wave_c_max = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) ? 24u : 64u; a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.fanout = e.fanout; a.fcap = e.fcap; a.PAIRS = e.PAIRS;
+  a.record = record ? 1 : 0;
+  const size_t lds = round_wg_lds_bytes(e.N, e.fcap, e.ASZP);
+  hipError_t r;
+  GS_ASZP_DISPATCH(e.ASZP, {
+    r = hipFuncSetAttribute((const void*)k_round_wg<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL(k_round_wg<A>, dim3(e.S), dim3(RWG_THREADS), lds, e.st, a);
+  });
+  return hipGetLastError();
+}
+
+}  // namespace gs

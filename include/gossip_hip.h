@@ -47,7 +47,7 @@ typedef enum gs_status {
 
 enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24) - 1, GS_HOP_UNREACHED = 0xFF };
 enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2 };
-enum { GS_FLAG_PROFILE = 1 };
+enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4 };
 
 typedef struct gs_params {
   uint32_t push_fanout;         /* Config::gossip_push_fanout (gossip.rs:113) */
@@ -57,7 +57,12 @@ typedef struct gs_params {
   int32_t device;               /* HIP device ordinal */
   uint32_t bfs_mode;            /* GS_BFS_* (results are identical in every mode) */
   uint32_t inbound_capacity;    /* per-(slot,node) inbound records per round; 0 = 64 */
-  uint32_t flags;               /* GS_FLAG_PROFILE: time kernels with hipEvents */
+  uint32_t flags;               /* GS_FLAG_PROFILE: time kernels with hipEvents; GS_FLAG_SPLIT_ROUND:
+                                   gs_round launches the step kernels instead of the one-kernel
+                                   workgroup round (same results; for A/B measurement);
+                                   GS_FLAG_NARROW_WAVE_PATH: the one-kernel round sends in-degrees
+                                   > 24 (not > 64) to its ordered single-lane consume (same results;
+                                   lets small test clusters cover that path) */
 } gs_params;
 
 typedef struct gs_slot {
@@ -147,6 +152,9 @@ int gs_read_failed(gs_engine* e, uint32_t slot, uint8_t* failed /*[n]*/);
 int gs_kernel_time(gs_engine* e, const char* family, double* ms, uint64_t* launches);
 int gs_kernel_time_reset(gs_engine* e);
 int gs_engine_info(gs_engine* e, uint32_t* n_nodes, uint32_t* n_slots, uint32_t* bfs_mode, uint64_t* device_bytes);
+/* 1 if gs_round runs the one-kernel workgroup round (BFS, consume, prune and
+ * statistics per slot in one workgroup), 0 if it launches the step kernels. */
+int gs_engine_round_kind(gs_engine* e, uint32_t* fused);
 
 /* --- host-side statistics (gossip_stats.rs), f64 in the reference's order --- */
 typedef struct gs_hops_stat { double mean, median; uint64_t max, min; } gs_hops_stat;

@@ -280,3 +280,95 @@ def test_large_network_invariants():
         reached = np.diff(off) > 0
         assert (first.astype(np.int64) == h[reached]).all()
         assert (dest >= 0).all()
+
+
+# ------------------------------------------- one-kernel workgroup round ----
+def run_fused_parity(n, S, rounds, *, fanout=6, asz=12, p=0.02, thr=0.15, mi=2, seed=11, check=(0, 1, 2, 3),
+                     fail_at=None, fraction=0.0, full_every=5, narrow=False):
+    """gs_round's one-kernel workgroup round against the oracle, round by round, on
+    `check` slots of an S-slot engine (the other slots run alongside)."""
+    pks, st = eb.synth.network(n)
+    eng = gs.Engine(st, S, fanout=fanout, active_set_size=asz, rotation_probability=p, seed=seed,
+                    bfs_mode=gs.GS_BFS_WORKGROUP, narrow_wave_path=narrow)
+    assert eng.info()["fused_round"]
+    origins = [(k * 37 + 1) % n for k in range(S)]
+    eng.set_slots(origins, mi, thr)
+    eng.init_active_sets()
+    sims = {k: ob.Sim(ob.PHILOX, seed, pks, st, fanout) for k in check}
+    for s in sims.values():
+        s.init_philox(asz)
+    total_prunes, max_in = 0, 0
+    for r in range(rounds):
+        if fail_at is not None and r == fail_at:
+            eng.fail_nodes([fraction] * S)
+            for s in sims.values():
+                s.fail_nodes(fraction)
+        eng.round(r, record=r >= 3)
+        for k, s in sims.items():
+            o = origins[k]
+            s.run_gossip(o)
+            s.consume_messages(o)
+            s.send_prunes(o, thr, mi)
+            np.testing.assert_array_equal(eng.distances(k), s.distances(), err_msg=f"hops slot {k} round {r}")
+            assert eng.prunes(k) == s.prunes(), f"prunes slot {k} round {r}"
+            total_prunes += len(s.prunes())
+            s.prune_connections()
+            e, i, pr = eng.counters(k)
+            oe, oi, op = s.counters()
+            np.testing.assert_array_equal(e, np.where(oe == U64MAX, 0, oe))
+            np.testing.assert_array_equal(i, np.where(oi == U64MAX, 0, oi))
+            np.testing.assert_array_equal(pr, op)
+            max_in = max(max_in, int(i.max()))
+            if r % full_every == 0 or r == rounds - 1:
+                up, ln, keys, sc = eng.caches(k)
+                oup, oln, okeys, osc = s.caches(o)
+                has = oup != 0xFFFFFFFF
+                np.testing.assert_array_equal(up[has], oup[has])
+                np.testing.assert_array_equal(ln, oln)
+                np.testing.assert_array_equal(keys, okeys)
+                np.testing.assert_array_equal(sc, osc)
+            s.chance_to_rotate(asz, p, r)  # the engine's round ends with the rotation
+            if r % full_every == 0 or r == rounds - 1:
+                np.testing.assert_array_equal(eng.pruned_all(k), s.pruned_all(o), err_msg=f"prune state {r}")
+    return eng, total_prunes, max_in
+
+
+def test_fused_round_parity():
+    """C2-shaped (all-origins batch) fused rounds: 45 rounds across two prune waves."""
+    eng, total, _ = run_fused_parity(300, 96, 45, check=(0, 5, 50, 95))
+    assert total > 0
+    with pytest.raises(gs.GsError):  # inbound records stay on-chip in the fused round
+        eng.inbound_lists(0)
+
+
+def test_fused_round_heavy_paths():
+    """fanout = active set = 32 on 150 nodes: in-degrees > 16 (wave path) and > 24
+    (ordered single-lane path, narrowed from > 64), cache entries > 32 keys (wave
+    prune), failures."""
+    eng, total, max_in = run_fused_parity(150, 64, 42, fanout=32, asz=32, p=0.05, thr=0.05, mi=1,
+                                          check=(0, 7, 33), fail_at=25, fraction=0.2, full_every=3, narrow=True)
+    assert total > 0
+    assert max_in > 24
+
+
+def test_fused_round_matches_split_round():
+    """One-kernel round == split kernels (WG BFS + consume/prune + stats) incl. summaries."""
+    pks, st = eb.synth.network(400)
+    engines = [gs.Engine(st, 80, seed=5, rotation_probability=0.03, bfs_mode=gs.GS_BFS_WORKGROUP, split_round=f)
+               for f in (False, True)]
+    assert engines[0].info()["fused_round"] and not engines[1].info()["fused_round"]
+    for e in engines:
+        e.set_slots([(k * 5) % 400 for k in range(80)], 2, 0.15)
+        e.init_active_sets()
+    for r in range(50):
+        for e in engines:
+            e.round(r, record=r >= 5)
+    a, b = engines
+    np.testing.assert_array_equal(a.summaries(), b.summaries())
+    for k in (0, 13, 79):
+        np.testing.assert_array_equal(a.hops(k), b.hops(k))
+        np.testing.assert_array_equal(a.pruned_all(k), b.pruned_all(k))
+        for x, y in zip(a.caches(k), b.caches(k)):
+            np.testing.assert_array_equal(x, y)
+        for x, y in zip(a.accumulators(k), b.accumulators(k)):
+            np.testing.assert_array_equal(x, y)
