@@ -164,6 +164,10 @@ def main():
     if os.environ.get("GS_PHASE_PROFILE") == "1" and fused:  # workgroup-ms per k_round_wg phase
         names = ["init", "bfs", "csr_stats", "consume_prune", "heavy", "summary"]
         phases = {nm: round(eng.kernel_time("phase." + chr(65 + i))[0], 2) for i, nm in enumerate(names)}
+        phases["bfs_levels_per_slot_round"] = round(eng.kernel_time("phase.H")[0] * 1e5 / (S * args.steps), 2)
+        lv = eng.kernel_time("phase.H")[0] * 1e5
+        for i, nm in enumerate(["lvl_row_load_cyc", "lvl_push_cyc", "lvl_rest_iters_cyc", "lvl_barriers_cyc"]):
+            phases[nm] = round(eng.kernel_time("phase." + chr(73 + i))[0] * 1e5 / max(lv, 1), 1)  # per level
     out = {
         "metric": METRIC,
         "value": E_all / dt,

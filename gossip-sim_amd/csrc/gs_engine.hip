@@ -213,7 +213,7 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   e->sum_cap = 64;
   ALLOC(e->sum, (size_t)e->sum_cap * S, 0);
   ALLOC(e->err, 4, 0);
-  if (const char* pp = std::getenv("GS_PHASE_PROFILE"); pp && pp[0] == '1') ALLOC(e->phase_clk, 8, 0);
+  if (const char* pp = std::getenv("GS_PHASE_PROFILE"); pp && pp[0] == '1') ALLOC(e->phase_clk, 16, 0);
 
   // stakes, buckets and the static rotation prefix sums
   std::vector<uint8_t> b(N);
@@ -745,8 +745,8 @@ int gs_kernel_time(gs_engine* eh, const char* family, double* ms, uint64_t* laun
     *ms = 0;
     *launches = 0;
     const int ph = family[6] - 'A';
-    if (!e->phase_clk || ph < 0 || ph >= 8) return GS_OK;
-    unsigned long long v[8];
+    if (!e->phase_clk || ph < 0 || ph >= 16) return GS_OK;
+    unsigned long long v[16];
     HIPC(hipMemcpy(v, e->phase_clk, sizeof(v), hipMemcpyDeviceToHost));
     *ms = (double)v[ph] * 1e-5;
     *launches = e->timers["round"].n;
@@ -780,7 +780,7 @@ int gs_kernel_time_reset(gs_engine* eh) {
     kv.second.ms = 0;
     kv.second.n = 0;
   }
-  if (e->phase_clk) HIPC(hipMemsetAsync(e->phase_clk, 0, 64, e->st));
+  if (e->phase_clk) HIPC(hipMemsetAsync(e->phase_clk, 0, 128, e->st));
   return GS_OK;
 }
 

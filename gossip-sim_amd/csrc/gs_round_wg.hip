@@ -86,7 +86,7 @@ struct RoundArgs {
 
 // LDS carve-up (byte offsets), shared by the host's size query and the kernel.
 struct RwgLayout {
-  uint32_t ctrl, hist, scr, cnt, qo, pm, nl, hops, bm, rec, total;
+  uint32_t ctrl, hist, scr, cnt, qo, pm, mk, nl, hops, bm, rec, total;
 };
 // pmw: bytes per push mask (2 when the ring has <= 16 slots)
 __host__ __device__ inline RwgLayout rwg_layout(uint32_t N, uint32_t fcap, uint32_t pmw) {
@@ -95,9 +95,10 @@ __host__ __device__ inline RwgLayout rwg_layout(uint32_t N, uint32_t fcap, uint3
   L.ctrl = o; o += 32 * 4;
   L.hist = o; o += 256 * 4;
   L.scr = o;  o += RWG_WAVES * RWG_SCR * 4;
-  L.cnt = o;  o += 4 * N;                       // in-degree (u32 atomics)
+  L.cnt = o;  o += 4 * ((N + 1) / 2);           // in-degree u16 (atomics on the containing u32)
   L.qo = o;   o += 4 * N;                       // BFS queues 2 x u16[N], then segment ends u32[N]
   L.pm = o;   o += (pmw * N + 3) & ~3u;         // push masks, then the heavy-node list u16[N]
+  L.mk = o;   o += (pmw * N + 3) & ~3u;         // the slot's prune masks, staged for the BFS
   L.nl = o;   o += (2 * N + 3) & ~3u;           // per node: ring head | len << 5 | entry bucket << 11
   L.hops = o; o += (N + 3) & ~3u;
   L.bm = o;   o += ((N + 31) / 32) * 4;         // stranded bitmap over stake rank
@@ -109,6 +110,14 @@ __host__ __device__ inline RwgLayout rwg_layout(uint32_t N, uint32_t fcap, uint3
 size_t round_wg_lds_bytes(uint32_t N, uint32_t fcap, uint32_t ASZP) {
   return rwg_layout(N, fcap, ASZP <= 16 ? 2 : 4).total;
 }
+
+// Streaming per-pair state (read or written once per round, ~0.5 GB/round at C2)
+// goes through non-temporal loads/stores so that it does not evict the shared
+// active-set rows (3.6 MB at C2) from L2.
+template <class T>
+__device__ inline T ntl(const T* p) { return __builtin_nontemporal_load(p); }
+template <class T>
+__device__ inline void nts(T* p, T v) { __builtin_nontemporal_store(v, p); }
 
 // ctrl words
 enum { C_QN = 0, C_NEXT = 1, C_ERR = 2, C_SEG = 3, C_VIS = 4, C_PUSH = 5, C_STR = 6, C_PRUNES = 7, C_SSUM = 8,
@@ -155,7 +164,7 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
   for (uint32_t i0 = 0; i0 < wl; i0 += 8) {
     uint32_t kc[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) kc[t] = i0 + t < wl ? (a.ckey + (size_t)(i0 + t) * PAIRS)[q] : 0xFFFFFFFEu;
+    for (int t = 0; t < 8; ++t) kc[t] = i0 + t < wl ? ntl(&(a.ckey + (size_t)(i0 + t) * PAIRS)[q]) : 0xFFFFFFFEu;
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
@@ -179,8 +188,8 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
       const uint32_t s0 = *sp & 0x7Fu;
       *sp = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
     } else if (len < CACHE_CAP) {
-      (a.ckey + (size_t)len * PAIRS)[q] = rk[j] & 0xFFFFu;
-      (a.cscore + (size_t)len * PAIRS)[q] = 1;
+      nts(&(a.ckey + (size_t)len * PAIRS)[q], rk[j] & 0xFFFFu);
+      nts(&(a.cscore + (size_t)len * PAIRS)[q], (uint8_t)1);
       ++len;
     } else {
       errf |= ERR_CACHE;
@@ -189,8 +198,8 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
 #pragma unroll
   for (int j = 2; j < 16; ++j) {  // rank order; inserted only while len < 50 (received_cache.rs:91-97)
     if ((uint32_t)j < c && !((present >> j) & 1u) && len < CACHE_LIMIT) {
-      (a.ckey + (size_t)len * PAIRS)[q] = rk[j] & 0xFFFFu;
-      (a.cscore + (size_t)len * PAIRS)[q] = 0;
+      nts(&(a.ckey + (size_t)len * PAIRS)[q], rk[j] & 0xFFFFu);
+      nts(&(a.cscore + (size_t)len * PAIRS)[q], (uint8_t)0);
       ++len;
     }
   }
@@ -211,8 +220,8 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, size_t base, const uin
       kk[i] = 0;
       ss[i] = 0;
       if ((uint32_t)i < wl) {
-        kk[i] = (a.ckey + (size_t)i * PAIRS)[q];
-        ss[i] = (a.cscore + (size_t)i * PAIRS)[q];
+        kk[i] = ntl(&(a.ckey + (size_t)i * PAIRS)[q]);
+        ss[i] = ntl(&(a.cscore + (size_t)i * PAIRS)[q]);
       }
     }
     asm volatile("" ::: "memory");
@@ -239,8 +248,8 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, size_t base, const uin
       if (tail && first == len) first = (uint32_t)i;
       const bool pruned = tail && node != org;
       npr += pruned;
-      (a.ckey + (size_t)i * PAIRS)[q] = node;
-      (a.cscore + (size_t)i * PAIRS)[q] = (uint8_t)((0x7Fu - (sk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
+      nts(&(a.ckey + (size_t)i * PAIRS)[q], node);
+      nts(&(a.cscore + (size_t)i * PAIRS)[q], (uint8_t)((0x7Fu - (sk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u)));
       cum = sat_add(cum, st);
     }
   }
@@ -410,9 +419,9 @@ __device__ inline void finish_node(const RoundArgs& a, size_t p, uint32_t meta, 
   uint32_t nm;
   if (pruned_now) nm = len << 16;  // std::mem::take: entry reset, pruned keys kept readable
   else nm = len | (up << 8);
-  if (nm != meta) a.cmeta[p] = nm;
+  if (nm != meta) nts(&a.cmeta[p], nm);
   const uint32_t npr = pruned_now ? npr_if_pruned : 0u;
-  a.prune_round[p] = (uint8_t)(npr < 255 ? npr : 255);
+  nts(&a.prune_round[p], (uint8_t)(npr < 255 ? npr : 255));
   if (a.record && npr) a.prune_acc[p] += npr;
 }
 
@@ -502,7 +511,8 @@ __global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
   const RwgLayout L = rwg_layout(N, a.fcap, (uint32_t)sizeof(PMT));
   uint32_t* ctrl = reinterpret_cast<uint32_t*>(smem + L.ctrl);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem + L.hist);
-  uint32_t* cnt_l = reinterpret_cast<uint32_t*>(smem + L.cnt);
+  uint32_t* cntw = reinterpret_cast<uint32_t*>(smem + L.cnt);
+  const uint16_t* cnt_l = reinterpret_cast<const uint16_t*>(smem + L.cnt);
   uint16_t* q0 = reinterpret_cast<uint16_t*>(smem + L.qo);
   uint16_t* q1 = q0 + N;
   uint32_t* off_l = reinterpret_cast<uint32_t*>(smem + L.qo);
@@ -510,6 +520,7 @@ __global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
   uint16_t* hv_l = reinterpret_cast<uint16_t*>(smem + L.pm);  // heavy nodes: consume from the front,
                                                               // prune-only from the back
   uint16_t* nl_l = reinterpret_cast<uint16_t*>(smem + L.nl);
+  PMT* mk_l = reinterpret_cast<PMT*>(smem + L.mk);
   uint8_t* hops_l = smem + L.hops;
   uint32_t* bm_l = reinterpret_cast<uint32_t*>(smem + L.bm);
   uint16_t* rec_l = reinterpret_cast<uint16_t*>(smem + L.rec);
@@ -523,10 +534,11 @@ __global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
   uint32_t errf = 0;
   unsigned long long t_mark = a.phase_clk && tid == 0 ? wall_clock64() : 0;
 
+  for (uint32_t i = tid; i < (N + 1) / 2; i += RWG_THREADS) cntw[i] = 0;
   for (uint32_t v = tid; v < N; v += RWG_THREADS) {
-    cnt_l[v] = 0;
     hops_l[v] = 0xFF;
     pm_l[v] = 0;
+    mk_l[v] = (PMT)ntl(&a.mask[base + v]);
     const uint32_t b = min((uint32_t)a.bucket[v], ob);  // entry the origin uses (push_active_set.rs:38-52)
     const uint32_t hv = a.hl[v * NB + b];
     nl_l[v] = (uint16_t)((hv & 0x1Fu) | ((hv >> 8) << 5) | (b << 11));
@@ -540,19 +552,21 @@ __global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
   RWG_MARK(0);
 
   // ---------------- A: BFS -------------------------------------------------
+  unsigned long long prof[5] = {0, 0, 0, 0, 0};  // profiling builds of the run only (thread 0)
   uint16_t* cur = q0;
   uint16_t* nxt = q1;
   for (uint32_t d = 0;; ++d) {
     const uint32_t qn = ctrl[C_QN];
     if (qn == 0) break;
     if (d + 1 >= 255) { errf |= ERR_DEPTH; break; }
+    unsigned long long tl0 = (a.phase_clk && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
     for (uint32_t i0 = 0; i0 < qn; i0 += RWG_THREADS) {
       const bool valid = i0 + tid < qn;
       uint32_t row[ASZP];
       uint32_t pushm = 0;
       if (valid) {
         const uint32_t u = cur[i0 + tid];
-        const uint32_t pmask = a.mask[base + u];
+        const uint32_t pmask = mk_l[u];
         const uint32_t nl = nl_l[u];
         load_row<ASZP>(a.peers + (size_t)(u * NB + (nl >> 11)) * ASZP, row);
         pushm = taken_slots<ASZP>(row, nl & 31u, (nl >> 5) & 63u, a.ASZ, pmask, org, a.fanout);
@@ -562,13 +576,26 @@ __global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
             if (((pushm >> s) & 1u) && a.frank[row[s]] < nf) pushm &= ~(1u << s);
         }
         pm_l[u] = (PMT)pushm;
+        if (a.phase_clk && tid == 0 && i0 == 0) {
+          const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+          prof[0] += t1 - tl0;  // level start -> row loaded (shader cycles)
+          tl0 = t1;
+        }
       } else {
 #pragma unroll
         for (int s = 0; s < ASZP; ++s) row[s] = 0;
       }
+      // All ring slots issue their LDS atomic back to back (slots not pushed add 0
+      // to a per-lane dummy word), then one wait: a conditional atomic per slot
+      // would be followed by its own lgkmcnt(0) wait.
       uint32_t old[ASZP];
+      uint32_t* dummy = scr + lane;
 #pragma unroll
-      for (int s = 0; s < ASZP; ++s) old[s] = ((pushm >> s) & 1u) ? atomicAdd(&cnt_l[row[s]], 1u) : 1u;
+      for (int s = 0; s < ASZP; ++s) {
+        const bool pu = (pushm >> s) & 1u;
+        const uint32_t w = row[s], sh = (w & 1u) << 4;
+        old[s] = (atomicAdd(pu ? &cntw[w >> 1] : dummy, pu ? 1u << sh : 0u) >> sh) & 0xFFFFu;
+      }
       uint32_t newm = 0;
 #pragma unroll
       for (int s = 0; s < ASZP; ++s)
@@ -581,13 +608,34 @@ __global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
 #pragma unroll
       for (int s = 0; s < ASZP; ++s)
         if ((newm >> s) & 1u) nxt[idx++] = (uint16_t)row[s];
+      if (a.phase_clk && tid == 0 && i0 == 0) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        prof[1] += t1 - tl0;  // row loaded -> pushes done
+        tl0 = t1;
+      }
+    }
+    if (a.phase_clk && tid == 0) {
+      const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+      prof[2] += t1 - tl0;  // remaining iterations of the level
+      tl0 = t1;
     }
     __syncthreads();
     if (tid == 0) { ctrl[C_QN] = ctrl[C_NEXT]; ctrl[C_NEXT] = 0; }
     uint16_t* t = cur; cur = nxt; nxt = t;
     __syncthreads();
+    if (a.phase_clk && tid == 0) {
+      prof[4] += 1;  // levels
+      prof[3] += __builtin_amdgcn_s_memtime() - tl0;  // the two barriers
+    }
   }
 
+  if (a.phase_clk && tid == 0) {
+    atomicAdd(&a.phase_clk[8], prof[0]);
+    atomicAdd(&a.phase_clk[9], prof[1]);
+    atomicAdd(&a.phase_clk[10], prof[2]);
+    atomicAdd(&a.phase_clk[11], prof[3]);
+    atomicAdd(&a.phase_clk[7], prof[4]);
+  }
   RWG_MARK(1);
   // ---------------- B: inbound CSR, per-pair outputs, round statistics ------
   for (uint32_t v0 = 0; v0 < N; v0 += RWG_THREADS) {  // segment per destination (order free)
@@ -609,18 +657,18 @@ __global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
       const uint32_t h = hops_l[v], c = cnt_l[v];
       const uint32_t pmv = h != 0xFF ? pm_l[v] : 0u;
       const uint32_t eg = __popc(pmv);
-      a.hops[p] = (uint8_t)h;
-      a.cnt[p] = c;
-      a.egress[p] = (uint8_t)eg;
+      nts(&a.hops[p], (uint8_t)h);
+      nts(&a.cnt[p], c);
+      nts(&a.egress[p], (uint8_t)eg);
       if (a.record) {  // measured-round statistics (gossip_main.rs:480-514)
         pushes += c;
-        if (c) a.ingress_acc[p] += c;
-        if (eg) a.egress_acc[p] += eg;
+        if (c) atomicAdd(&a.ingress_acc[p], c);  // fire-and-forget: no load round trip
+        if (eg) atomicAdd(&a.egress_acc[p], eg);
         if (h != 0xFF) {
           ++vis;
           atomicAdd(&hist[h], 1u);
         } else if (!(nf && a.frank[v] < nf)) {
-          a.strand[p] += 1;
+          atomicAdd(&a.strand[p], 1u);
           ++sc;
           ss += a.stake[v];
           const uint32_t r = a.srank[v];
@@ -630,9 +678,16 @@ __global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
       if (pmv) {
         uint32_t row[ASZP];
         load_row<ASZP>(a.peers + (size_t)(v * NB + (nl_l[v] >> 11)) * ASZP, row);
+        uint32_t pos[ASZP];
+        uint32_t* dummy = scr + lane;
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s) {
+          const bool pu = (pmv >> s) & 1u;
+          pos[s] = atomicAdd(pu ? &off_l[row[s]] : dummy, pu ? 1u : 0u);
+        }
 #pragma unroll
         for (int s = 0; s < ASZP; ++s)
-          if ((pmv >> s) & 1u) rec_l[atomicAdd(&off_l[row[s]], 1u)] = (uint16_t)v;
+          if ((pmv >> s) & 1u) rec_l[pos[s]] = (uint16_t)v;
       }
     }
     if (a.record) {
@@ -650,19 +705,21 @@ __global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
   const double thr = a.thr[o];
   const uint64_t so = a.stake[org];
   uint32_t npr_sum = 0;
+  uint32_t meta_next = tid < N ? ntl(&a.cmeta[base + tid]) : 0u;
   for (uint32_t v = tid; v < N; v += RWG_THREADS) {
     const size_t p = base + v;
+    const uint32_t meta = meta_next;  // the next node's meta is in flight while this one is consumed
+    if (v + RWG_THREADS < N) meta_next = ntl(&a.cmeta[p + RWG_THREADS]);
     const uint32_t c = cnt_l[v];
     if (c > LANE_C) {
       hv_l[atomicAdd(&ctrl[C_NHC], 1u)] = (uint16_t)v;
       continue;
     }
-    const uint32_t meta = a.cmeta[p];
     uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
     if (c) consume_lane(a, p, rec_l + (off_l[v] - c), hops_l, c, len, up, errf);
     if (up >= MIN_NUM_UPSERTS) {
       if (len > LANE_L) {
-        a.cmeta[p] = len | (up << 8);
+        nts(&a.cmeta[p], len | (up << 8));
         hv_l[N - 1 - atomicAdd(&ctrl[C_NHP], 1u)] = (uint16_t)v;
         continue;
       }
