@@ -43,6 +43,18 @@ def load_pkg():
     return mod
 
 
+def pmc_traffic(kernel, nodes, slots):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary of
+    this same workload (scripts/pmc.sh + scripts/pmc_summary.py), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{kernel}_{nodes}x{slots}.json")),
+                       reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(pks, stakes, args, budget_s):
     """Oracle (port of the reference path) on host cores: one origin-sim, rounds until the budget."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -153,10 +165,12 @@ def main():
     roof = None
     if k_ms > 0:
         achieved = b_kernel / (k_ms * 1e-3) / 1e9
+        kname = "k_round_wg" if fused else \
+            ("k_bfs_wg" if eng.info()["bfs_mode"] == gs.GS_BFS_WORKGROUP else "k_bfs_level")
+        traffic, tsrc = pmc_traffic(kname, args.nodes, S)
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "k_round_wg" if fused else
-                          ("k_bfs_wg" if eng.info()["bfs_mode"] == gs.GS_BFS_WORKGROUP else "k_bfs_level"),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+                "kernel": kname,
                 "bytes_model": "B_prop+B_consume+B_stats (SURVEY 8d)" if fused else "B_prop (SURVEY 8d)",
                 "bytes_per_launch": round(b_kernel / max(k_n, 1)), "avg_launch_us": round(k_ms * 1e3 / max(k_n, 1), 2),
                 "launches": k_n}

@@ -18,6 +18,8 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libgossip_hip.so")
+if os.environ.get("GS_LIB_VARIANT"):  # A/B builds of the same sources (scripts/), never a fallback
+    LIB_PATH = os.path.join(PKG_DIR, "variants", os.environ["GS_LIB_VARIANT"], "libgossip_hip.so")
 
 GS_BFS_AUTO, GS_BFS_WORKGROUP, GS_BFS_LEVEL = 0, 1, 2
 GS_FLAG_PROFILE = 1

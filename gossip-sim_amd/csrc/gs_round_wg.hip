@@ -29,6 +29,9 @@
 
 namespace gs {
 
+#ifndef RWG_MIN_WAVES
+#define RWG_MIN_WAVES 4  // waves per SIMD (VGPR budget 128); LDS allows 2 workgroups per CU at C2
+#endif
 constexpr uint32_t RWG_THREADS = 512;
 constexpr uint32_t RWG_WAVES = RWG_THREADS / 64;
 constexpr uint32_t RWG_SCR = 128;  // per-wave LDS scratch (u32): staged cache keys / prune keys
@@ -504,7 +507,7 @@ __device__ inline void wave_hop_stats(const uint32_t* hist, uint32_t* ctrl) {
 }
 
 template <int ASZP>
-__global__ __launch_bounds__(RWG_THREADS, 4) void k_round_wg(RoundArgs a) {
+__global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundArgs a) {
   using PMT = typename std::conditional<(ASZP <= 16), uint16_t, uint32_t>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t N = a.N;

@@ -29,3 +29,9 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline
   find gpurun_out/prof -name "*stats*" | head
 fi
+if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
+  # HBM traffic of the round kernel over the bench's own default timed steps
+  BENCH_ARGS="--steps 100 --warmup 20 --no-cpu-baseline --no-profile" bash scripts/pmc.sh fetch:FETCH_SIZE write:WRITE_SIZE || exit $?
+  python3 scripts/pmc_summary.py --kernel k_round_wg --launches 100 --bench-args "--steps 100 --warmup 20" \
+    --out gpurun_out/pmc_k_round_wg_3000x3000.json
+fi
