@@ -165,8 +165,8 @@ def main():
     roof = None
     if k_ms > 0:
         achieved = b_kernel / (k_ms * 1e-3) / 1e9
-        kname = "k_round_wg" if fused else \
-            ("k_bfs_wg" if eng.info()["bfs_mode"] == gs.GS_BFS_WORKGROUP else "k_bfs_level")
+        kname = "k_round_wg" if fused else {gs.GS_BFS_WORKGROUP: "k_bfs_wg", gs.GS_BFS_LEVEL: "k_bfs_level",
+                                            gs.GS_BFS_BINNED: "k_bin_expand+k_bin_apply"}[eng.info()["bfs_mode"]]
         traffic, tsrc = pmc_traffic(kname, args.nodes, S)
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,

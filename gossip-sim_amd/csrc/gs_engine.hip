@@ -152,12 +152,21 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
 
   uint32_t mode = prm->bfs_mode;
   const size_t lds = bfs_wg_lds_bytes(n);
-  if (mode == GS_BFS_AUTO) mode = (n <= 8192 && n_slots >= 64) ? GS_BFS_WORKGROUP : GS_BFS_LEVEL;
+  const size_t pairs = (size_t)n * n_slots;
+  if (mode == GS_BFS_AUTO)
+    mode = (n <= 8192 && n_slots >= 64) ? GS_BFS_WORKGROUP : (pairs <= (1ull << 28) ? GS_BFS_BINNED : GS_BFS_LEVEL);
+  if (mode == GS_BFS_BINNED && pairs > (1ull << 28)) {
+    destroy_engine(e);
+    return fail(GS_EINVAL, "binned BFS supports n_nodes * n_slots <= 2^28");
+  }
   if (mode == GS_BFS_WORKGROUP && (n > 65535 || lds > 160 * 1024)) {
     destroy_engine(e);
     return fail(GS_EINVAL, "workgroup BFS needs the per-slot state (9 B/node) to fit in 160 KiB of LDS");
   }
-  if (mode != GS_BFS_WORKGROUP && mode != GS_BFS_LEVEL) { destroy_engine(e); return fail(GS_EINVAL, "bfs_mode"); }
+  if (mode != GS_BFS_WORKGROUP && mode != GS_BFS_LEVEL && mode != GS_BFS_BINNED) {
+    destroy_engine(e);
+    return fail(GS_EINVAL, "bfs_mode");
+  }
   e->bfs_mode = mode;
   // one-kernel round (gs_round): per-slot state in LDS, at most 160 KiB per workgroup
   e->fused = mode == GS_BFS_WORKGROUP && !(prm->flags & GS_FLAG_SPLIT_ROUND) &&
@@ -194,9 +203,19 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   ALLOC(e->ingress_acc, PAIRS, 0);
   ALLOC(e->prune_acc, PAIRS, 0);
   ALLOC(e->strand, PAIRS, 0);
-  if (mode == GS_BFS_LEVEL) {
+  if (mode == GS_BFS_LEVEL || mode == GS_BFS_BINNED) {
     ALLOC(e->q[0], PAIRS, 0);
     ALLOC(e->q[1], PAIRS, 0);
+  }
+  if (mode == GS_BFS_BINNED) {  // ~512 bins of 2^BS consecutive pairs, BS in [10, 15]
+    uint32_t lg = 0;
+    while ((1ull << lg) < PAIRS) ++lg;
+    e->bin_BS = std::min(15u, std::max(10u, lg > 9 ? lg - 9 : 0u));
+    e->bin_nb = (uint32_t)((PAIRS + (1ull << e->bin_BS) - 1) >> e->bin_BS);
+    e->bin_G = (uint32_t)std::min<size_t>(1024, std::max<size_t>(32, PAIRS / 2048));
+    ALLOC(e->bin_pm, PAIRS, 0);
+    ALLOC(e->bin_area, PAIRS * e->fcap, 0);
+    ALLOC(e->bin_T, ((size_t)e->bin_nb + 1) * e->bin_G, 0);
   }
   ALLOC(e->lvl, 256, 0);
   ALLOC(e->rot_list, N, 0);

@@ -69,6 +69,11 @@ struct Engine {
   // level-synchronous BFS
   uint32_t* q[2] = {nullptr, nullptr};
   uint32_t* lvl = nullptr;  // frontier sizes per level [256]
+  // propagation-blocked BFS (GS_BFS_BINNED, gs_bfs_binned.hip)
+  uint32_t* bin_pm = nullptr;   // push mask per frontier position
+  uint2* bin_area = nullptr;    // push records (pair, src), PAIRS * fcap
+  uint32_t* bin_T = nullptr;    // [nbins + 1][G] segment starts
+  uint32_t bin_G = 0, bin_BS = 0, bin_nb = 0;
   // rotation
   uint32_t* rot_list = nullptr;
   uint32_t* rot_count = nullptr;
@@ -120,6 +125,7 @@ hipError_t launch_fail_keys(Engine& e, uint64_t* keys, uint32_t* ids);
 hipError_t launch_scatter_rank(Engine& e, const uint32_t* sorted_ids, uint32_t* rank_out);
 hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket, uint32_t bits);
 hipError_t launch_bfs(Engine& e, bool record);
+hipError_t launch_bfs_binned(Engine& e, bool record);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
 hipError_t launch_rotate(Engine& e, uint32_t round);
 hipError_t launch_stats(Engine& e, uint32_t rec_index, int mode);

@@ -46,7 +46,12 @@ typedef enum gs_status {
 } gs_status;
 
 enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24) - 1, GS_HOP_UNREACHED = 0xFF };
-enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2 };
+/* BFS strategies (results are identical): WORKGROUP = one workgroup per slot with
+ * LDS state (small clusters, many slots); LEVEL = level-synchronous over all
+ * slots with a global atomic per push; BINNED = level-synchronous,
+ * propagation-blocked (pushes binned by destination range, LDS counters per
+ * bin; large clusters). AUTO picks WORKGROUP, else BINNED, else LEVEL. */
+enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2, GS_BFS_BINNED = 3 };
 enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4 };
 
 typedef struct gs_params {

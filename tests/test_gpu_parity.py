@@ -17,7 +17,7 @@ gs = eb.gs
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 U64MAX = np.uint64(2**64 - 1)
-MODES = [gs.GS_BFS_WORKGROUP, gs.GS_BFS_LEVEL]
+MODES = [gs.GS_BFS_WORKGROUP, gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED]
 
 
 # ------------------------------------------------------------ reference KATs ----
@@ -172,9 +172,10 @@ def test_round_by_round_parity(mode):
     assert total > 0  # the ~20-round prune waves were exercised
 
 
-def test_parity_sweep_params_and_failures():
+@pytest.mark.parametrize("mode", [gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED])
+def test_parity_sweep_params_and_failures(mode):
     """Per-slot thresholds / min-ingress and fail-nodes (failed peers burn fanout slots)."""
-    run_parity(180, [1, 3, 5, 9], 42, p=0.03, mode=gs.GS_BFS_LEVEL, thr=[0.0, 0.15, 0.4, 1.0], mi=[0, 2, 3, 1],
+    run_parity(180, [1, 3, 5, 9], 42, p=0.03, mode=mode, thr=[0.0, 0.15, 0.4, 1.0], mi=[0, 2, 3, 1],
                fail_at=2, fractions=[0.1, 0.2, 0.3, 0.5], full_every=6)
 
 
@@ -280,6 +281,36 @@ def test_large_network_invariants():
         reached = np.diff(off) > 0
         assert (first.astype(np.int64) == h[reached]).all()
         assert (dest >= 0).all()
+
+
+def test_binned_bfs_matches_level_bfs_large():
+    """N = 300k, 3 slots, a fail-nodes fraction: the propagation-blocked BFS gives
+    the level BFS's hops, in-degrees, inbound sets, counters and summaries."""
+    n = 300_000
+    st = eb.synth.power_law_stakes(n)
+    engs = [gs.Engine(st, 3, seed=33, rotation_probability=0.01, bfs_mode=m)
+            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED)]
+    for e in engs:
+        e.set_slots([0, 17, n - 1], [2, 1, 3], [0.15, 0.3, 0.05])
+        e.init_active_sets()
+        e.fail_nodes([0.0, 0.2, 0.1])
+    for r in range(4):
+        for e in engs:
+            e.round(r, record=r >= 1)
+        a, b = engs
+        for k in range(3):
+            np.testing.assert_array_equal(a.hops(k), b.hops(k))
+            offa, srca, hopa = a.inbound(k, cap=8 * n)
+            offb, srcb, hopb = b.inbound(k, cap=8 * n)
+            np.testing.assert_array_equal(offa, offb)
+            np.testing.assert_array_equal(srca, srcb)  # lists come back in consume order
+            np.testing.assert_array_equal(hopa, hopb)
+            for x, y in zip(a.counters(k), b.counters(k)):
+                np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(engs[0].summaries(), engs[1].summaries())
+    for k in range(3):
+        for x, y in zip(engs[0].accumulators(k), engs[1].accumulators(k)):
+            np.testing.assert_array_equal(x, y)
 
 
 # ------------------------------------------- one-kernel workgroup round ----

@@ -1,0 +1,154 @@
+"""Sweeps sharded over ranks (gossip-sim_amd/sweep.py).
+
+CPU: world_size 2 over gloo, each rank's sims run by the oracle (test-only
+runner): the assembled results on every rank must equal a one-process run,
+bit for bit. GPU: the same with the HIP engine, two ranks sharing cuda:0.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+import engine_bind as eb
+
+gs = eb.gs
+import gossip_sim_amd.sweep as sweep  # noqa: E402
+
+N, ITERS, WARM = 90, 26, 6
+CFG = dict(fanout=6, asz=12, iterations=ITERS, warm_up=WARM, p=0.05, thr=0.15, min_ingress_nodes=2,
+           fraction_to_fail=0.1, when_to_fail=4, test_type=5, seed=7)
+FRACTIONS = [0.1, 0.2, 0.3, 0.45, 0.05]
+RANKS = [1, 1, 2, 1, 3]
+
+
+class _OracleResult:
+    def __init__(self, stats):
+        self.stats = stats
+
+    def f64(self, j, name):
+        return self.stats[j].f64(name)
+
+    def u64(self, j, name):
+        return self.stats[j].u64(name)
+
+
+def oracle_runner(stakes, *, n_sims, origin_ranks=None, min_ingress=None, thresholds=None, fractions=None,
+                  device=None, bfs_mode=None, **kw):
+    """Test-only runner with run_simulations' signature, backed by the CPU oracle."""
+    import oracle_bind as ob
+    pks, _ = eb.synth.network(len(stakes))
+    out = []
+    for j in range(n_sims):
+        out.append(ob.run_simulation(
+            pks, stakes, fanout=kw["fanout"], asz=kw["asz"], iterations=kw["iterations"],
+            origin_rank=origin_ranks[j] if origin_ranks else 1, p=kw["p"],
+            thr=thresholds[j] if thresholds else kw["thr"],
+            min_ingress=min_ingress[j] if min_ingress else kw["min_ingress_nodes"],
+            fraction_to_fail=fractions[j] if fractions else kw["fraction_to_fail"],
+            when_to_fail=kw["when_to_fail"], test_type=kw["test_type"], warm_up=kw["warm_up"], seed=kw["seed"]))
+    return _OracleResult(out)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _save(res, path):
+    arrs = {}
+    for i in range(res.n_sims):
+        for kind, name in sweep.NAMES:
+            a = res.f64(i, name) if kind == "f" else res.u64(i, name)
+            arrs[f"{kind}:{name}:{i}"] = a
+    np.savez(path, **arrs)
+
+
+def _worker(rank, world, port, outdir, use_gpu):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.dirname(here)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as tdist
+    import engine_bind  # noqa: F401  (registers gossip_sim_amd)
+    import gossip_sim_amd.sweep as sw
+    from test_sweep_dist import oracle_runner, FRACTIONS, RANKS, CFG, N
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    _, st = engine_bind.synth.network(N)
+    res = sw.run_sharded(st, n_sims=len(FRACTIONS), origin_ranks=RANKS, fractions=FRACTIONS,
+                         runner=None if use_gpu else oracle_runner, device=0 if use_gpu else None, **CFG)
+    _save(res, os.path.join(outdir, f"rank{rank}.npz"))
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def _run_world(world, use_gpu):
+    import torch.multiprocessing as mp
+    d = tempfile.mkdtemp()
+    mp.spawn(_worker, args=(world, _free_port(), d, use_gpu), nprocs=world, join=True)
+    return [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
+
+
+def _reference(use_gpu):
+    _, st = eb.synth.network(N)
+    if use_gpu:
+        res = gs.run_simulations(st, n_sims=len(FRACTIONS), origin_ranks=RANKS, fractions=FRACTIONS, **CFG)
+    else:
+        res = oracle_runner(st, n_sims=len(FRACTIONS), origin_ranks=RANKS, fractions=FRACTIONS, **CFG)
+    out = {}
+    for i in range(len(FRACTIONS)):
+        for kind, name in sweep.NAMES:
+            out[f"{kind}:{name}:{i}"] = res.f64(i, name) if kind == "f" else res.u64(i, name)
+    return out
+
+
+def _check(got, want):
+    assert set(got) == set(want)
+    for k in want:
+        g, w = got[k], want[k]
+        assert g.dtype == w.dtype and g.shape == w.shape, k
+        assert g.tobytes() == w.tobytes(), k  # bit-exact, f64 included
+
+
+def test_shard_partitions_units():
+    for n in (0, 1, 5, 13, 16):
+        for world in (1, 2, 3, 8):
+            owned = sorted(i for r in range(world) for i in sweep.shard(n, r, world))
+            assert owned == list(range(n))
+            sizes = [len(sweep.shard(n, r, world)) for r in range(world)]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_allreduce_single_process_roundtrip():
+    rng = np.random.default_rng(3)
+    local = {}
+    for i in range(3):
+        local[i] = {(k, nm): (rng.standard_normal(i + 2) if k == "f" else rng.integers(0, 2**63, i + 1,
+                                                                                        dtype=np.uint64))
+                    for k, nm in sweep.NAMES}
+    local[1][("f", "coverage")] = np.array([-0.0, np.nan, np.inf])
+    res = sweep.allreduce_results(local, 3)
+    for i in range(3):
+        for k, nm in sweep.NAMES:
+            a = res.f64(i, nm) if k == "f" else res.u64(i, nm)
+            assert a.tobytes() == local[i][(k, nm)].tobytes()
+
+
+def test_sharded_sweep_gloo_world2_matches_one_process():
+    want = _reference(use_gpu=False)
+    outs = _run_world(2, use_gpu=False)
+    for got in outs:  # every rank holds every sim after the all-reduce
+        _check(got, want)
+
+
+@pytest.mark.gpu
+def test_sharded_sweep_gpu_world2_matches_one_process():
+    want = _reference(use_gpu=True)
+    outs = _run_world(2, use_gpu=True)
+    for got in outs:
+        _check(got, want)
