@@ -51,7 +51,7 @@ struct BinArgs {
   uint32_t* pm;     // push mask per frontier position (pass 1 -> pass 2)
   uint2* area;      // push records (pair, src) per expand workgroup
   uint32_t* T;      // [nbins + 1][G] segment starts (row nbins = workgroup totals)
-  uint32_t N, ASZ, fanout, capin, G, BS, nbins;
+  uint32_t N, ASZ, fanout, capin, G, BS, nbins, qmin;
   size_t PAIRS;
   int record;
 };
@@ -82,10 +82,17 @@ __device__ inline uint32_t pair_pushes(const BinArgs& a, uint32_t p, uint32_t (&
   return pushm;
 }
 
-// Exclusive scan of LDS counts h[0..n) in place (whole workgroup); returns the total.
+constexpr uint32_t APPLY_THREADS = 256;
+// Levels with fewer frontier pairs than this run k_bfs_level (a global atomic per
+// push is cheap at that size; the binned pair of kernels has a fixed cost).
+// (GS_FLAG_BINNED_ALL_LEVELS: 0, every level binned -- lets small tests cover the kernels.)
+constexpr uint32_t BIN_MIN_FRONTIER = 1u << 17;
+
+// Exclusive scan of LDS counts h[0..n) in place (whole workgroup of THREADS); returns the total.
+template <uint32_t THREADS = BIN_THREADS>
 __device__ inline uint32_t block_excl_scan(uint32_t* h, uint32_t n, uint32_t* wsum) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint32_t per = (n + BIN_THREADS - 1) / BIN_THREADS;
+  const uint32_t per = (n + THREADS - 1) / THREADS;
   const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
   uint32_t s = 0;
   for (uint32_t i = lo; i < hi; ++i) s += h[i];
@@ -93,7 +100,7 @@ __device__ inline uint32_t block_excl_scan(uint32_t* h, uint32_t n, uint32_t* ws
   if (lane == 63) wsum[wid] = incl;
   __syncthreads();
   uint32_t wb = 0, tot = 0;
-  for (uint32_t k = 0; k < BIN_THREADS / 64; ++k) {
+  for (uint32_t k = 0; k < THREADS / 64; ++k) {
     if (k < wid) wb += wsum[k];
     tot += wsum[k];
   }
@@ -111,6 +118,7 @@ template <int ASZP>
 __global__ __launch_bounds__(BIN_THREADS) void k_bin_expand(BinArgs a, uint32_t d, const uint32_t* __restrict__ qcur) {
   extern __shared__ uint32_t hist[];  // [nbins] + 4 wave sums
   const uint32_t qn = a.lvl[d];
+  if (qn < a.qmin || qn == 0) return;
   uint32_t lo, hi;
   slice_of(qn, a.G, blockIdx.x, lo, hi);
   if (lo >= hi) return;  // apply derives the same slices and skips this workgroup
@@ -136,6 +144,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin_expand(BinArgs a, uint32_t 
   const uint32_t total = block_excl_scan(hist, nb, hist + nb);
   for (uint32_t b = tid; b < nb; b += BIN_THREADS) a.T[(size_t)b * a.G + w] = hist[b];
   if (tid == 0) a.T[(size_t)nb * a.G + w] = total;
+  __syncthreads();  // every segment start is published before pass 2 advances them
   // pass 2: records into the bin segments of this workgroup's area
   uint2* area = a.area + (size_t)lo * min(a.fanout, a.ASZ);
   for (uint32_t i = lo + tid; i < hi; i += BIN_THREADS) {
@@ -156,40 +165,78 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin_expand(BinArgs a, uint32_t 
   }
 }
 
-__global__ __launch_bounds__(BIN_THREADS) void k_bin_apply(BinArgs a, uint32_t d, uint32_t* __restrict__ qnxt) {
+// LDS of the apply kernel: segment prefix [G + 1], segment starts [G], the bin's
+// counters [BP] (u32 in-degrees when staged, else packed u16 arrival indices),
+// first arrivals u16 [BP], control words.
+__host__ __device__ inline size_t bin_apply_lds_words(uint32_t G, uint32_t BS) {
+  return 2 * (size_t)G + 1 + ((size_t)1 << BS) + ((size_t)1 << BS) / 2 + 24;
+}
+
+__global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t d, uint32_t* __restrict__ qnxt) {
   extern __shared__ uint32_t smem[];
   const uint32_t qn = a.lvl[d];
-  if (qn == 0) return;
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  if (qn < a.qmin || qn == 0) return;
+  const uint32_t tid = threadIdx.x, G = a.G;
   const uint32_t b = blockIdx.x, BP = 1u << a.BS;
-  uint32_t* cw = smem;                                         // BP u16 arrival counters
-  uint16_t* fl = reinterpret_cast<uint16_t*>(smem + BP / 2);   // first arrivals (bin-local), BP u16
-  uint32_t* ctl = smem + BP;                                   // [0] first-arrival count, [1] base, [2] overflow
-  for (uint32_t i = tid; i < BP / 2; i += BIN_THREADS) cw[i] = 0;
-  if (tid < 4) ctl[tid] = 0;
+  uint32_t* pre = smem;                                          // [G + 1]
+  uint32_t* sb = pre + G + 1;                                    // [G]
+  uint32_t* cw = sb + G;                                         // [BP]
+  uint16_t* fl = reinterpret_cast<uint16_t*>(cw + BP);           // [BP]
+  uint32_t* ctl = cw + BP + BP / 2;                              // [0] first arrivals, [1] base, [2] overflow, [4..19] scan
+  // 1. this bin's segment in every expand workgroup's area
+  for (uint32_t w = tid; w < G; w += APPLY_THREADS) {
+    uint32_t lo, hi, sz = 0, st = 0;
+    slice_of(qn, G, w, lo, hi);
+    if (lo < hi) {
+      st = a.T[(size_t)b * G + w];
+      sz = a.T[(size_t)(b + 1) * G + w] - st;
+    }
+    pre[w] = sz;
+    sb[w] = st;
+  }
+  if (tid < 3) ctl[tid] = 0;
   __syncthreads();
+  const uint32_t total = block_excl_scan<APPLY_THREADS>(pre, G, ctl + 4);
+  if (tid == 0) pre[G] = total;
   const uint32_t q0 = b << a.BS;
+  const uint32_t qend = (uint32_t)min((size_t)q0 + BP, a.PAIRS);
+  // 2. counters: a busy bin stages its in-degrees (one coalesced read and write);
+  //    a quiet one keeps per-level arrival indices and reads cnt[] per record
+  const bool staged = total >= BP / 4;
+  if (staged) {
+    for (uint32_t i = tid; i < BP; i += APPLY_THREADS) cw[i] = q0 + i < qend ? a.cnt[q0 + i] : 0u;
+  } else {
+    for (uint32_t i = tid; i < BP / 2; i += APPLY_THREADS) cw[i] = 0;
+  }
+  __syncthreads();
   const uint32_t fc = min(a.fanout, a.ASZ);
   const uint32_t hop = d + 1;
   bool overflow = false;
-  for (uint32_t w = tid; w < a.G; w += BIN_THREADS) {
-    uint32_t lo, hi;
-    slice_of(qn, a.G, w, lo, hi);
-    if (lo >= hi) continue;
-    const uint32_t s0 = a.T[(size_t)b * a.G + w], s1 = a.T[(size_t)(b + 1) * a.G + w];
-    const uint2* area = a.area + (size_t)lo * fc;
-    for (uint32_t j = s0; j < s1; ++j) {
-      const uint2 r = area[j];
-      const uint32_t q = r.x, ql = q - q0, sh = (ql & 1u) << 4;
+  // 3. one thread per record
+  for (uint32_t r = tid; r < total; r += APPLY_THREADS) {
+    uint32_t lo = 0, hi = G;  // largest w with pre[w] <= r (a non-empty segment)
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pre[mid] <= r) lo = mid; else hi = mid;
+    }
+    const uint32_t w = lo;
+    uint32_t wlo, whi;
+    slice_of(qn, G, w, wlo, whi);
+    const uint2 rec = a.area[(size_t)wlo * fc + sb[w] + (r - pre[w])];
+    const uint32_t q = rec.x, ql = q - q0;
+    uint32_t slot;
+    if (staged) {
+      slot = atomicAdd(&cw[ql], 1u);
+    } else {
+      const uint32_t sh = (ql & 1u) << 4;
       const uint32_t k = (atomicAdd(&cw[ql >> 1], 1u << sh) >> sh) & 0xFFFFu;
-      const uint32_t before = a.cnt[q];
-      const uint32_t slot = before + k;
-      if (slot < a.capin) a.inb[(size_t)slot * a.PAIRS + q] = (hop << 24) | r.y;
-      else overflow = true;
-      if (slot == 0) {  // first arrival: hop = dist[src] + 1 (gossip.rs:594-600)
-        a.hops[q] = (uint8_t)hop;
-        fl[atomicAdd(&ctl[0], 1u)] = (uint16_t)ql;
-      }
+      slot = a.cnt[q] + k;
+    }
+    if (slot < a.capin) a.inb[(size_t)slot * a.PAIRS + q] = (hop << 24) | rec.y;
+    else overflow = true;
+    if (slot == 0) {  // first arrival: hop = dist[src] + 1 (gossip.rs:594-600)
+      a.hops[q] = (uint8_t)hop;
+      fl[atomicAdd(&ctl[0], 1u)] = (uint16_t)ql;
     }
   }
   if (overflow) ctl[2] = 1;
@@ -197,18 +244,21 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin_apply(BinArgs a, uint32_t d
   const uint32_t nf = ctl[0];
   if (tid == 0 && nf) ctl[1] = atomicAdd(&a.lvl[d + 1], nf);
   if (tid == 0 && ctl[2]) atomicOr(a.err, ERR_INBOUND);
-  __syncthreads();
-  const uint32_t base = ctl[1];
-  for (uint32_t i = tid; i < nf; i += BIN_THREADS) qnxt[base + i] = q0 + fl[i];
-  // this level's arrivals into the bin's in-degree counters
-  const uint32_t qend = (uint32_t)min((size_t)q0 + BP, a.PAIRS);
-  for (uint32_t ql = 2 * tid; q0 + ql < qend; ql += 2 * BIN_THREADS) {
-    const uint32_t c2 = cw[ql >> 1];
-    if (!c2) continue;
-    if (c2 & 0xFFFFu) a.cnt[q0 + ql] += c2 & 0xFFFFu;
-    if ((c2 >> 16) && q0 + ql + 1 < qend) a.cnt[q0 + ql + 1] += c2 >> 16;
+  // 4. the bin's in-degrees after this level
+  if (staged) {
+    for (uint32_t i = tid; q0 + i < qend; i += APPLY_THREADS) a.cnt[q0 + i] = cw[i];
+  } else {
+    for (uint32_t ql = 2 * tid; q0 + ql < qend; ql += 2 * APPLY_THREADS) {
+      const uint32_t c2 = cw[ql >> 1];
+      if (!c2) continue;
+      if (c2 & 0xFFFFu) a.cnt[q0 + ql] += c2 & 0xFFFFu;
+      if ((c2 >> 16) && q0 + ql + 1 < qend) a.cnt[q0 + ql + 1] += c2 >> 16;
+    }
   }
-  (void)lane;
+  __syncthreads();
+  // 5. first arrivals join the next frontier
+  const uint32_t base = ctl[1];
+  for (uint32_t i = tid; i < nf; i += APPLY_THREADS) qnxt[base + i] = q0 + fl[i];
 }
 
 __global__ void k_bin_seed(BinArgs a, const uint32_t* __restrict__ origin, uint32_t S, uint32_t* q0) {
@@ -220,7 +270,6 @@ __global__ void k_bin_seed(BinArgs a, const uint32_t* __restrict__ origin, uint3
   if (o == 0) a.lvl[0] = S;
 }
 
-size_t bin_apply_lds_bytes(uint32_t BS) { return ((size_t)1 << BS) * 4 + 16; }
 
 hipError_t launch_bfs_binned(Engine& e, bool record) {
   BinArgs a;
@@ -229,22 +278,24 @@ hipError_t launch_bfs_binned(Engine& e, bool record) {
   a.egress_acc = e.egress_acc; a.lvl = e.lvl; a.err = e.err; a.pm = e.bin_pm; a.area = e.bin_area;
   a.T = e.bin_T; a.N = e.N; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.G = e.bin_G;
   a.BS = e.bin_BS; a.nbins = e.bin_nb; a.PAIRS = e.PAIRS; a.record = record ? 1 : 0;
+  a.qmin = (e.prm.flags & GS_FLAG_BINNED_ALL_LEVELS) ? 0u : BIN_MIN_FRONTIER;
   hipError_t r;
   if ((r = hipMemsetAsync(e.hops, 0xFF, e.PAIRS, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.cnt, 0, e.PAIRS * 4, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st)) != hipSuccess) return r;
   hipLaunchKernelGGL(k_bin_seed, dim3((e.S + 255) / 256), dim3(256), 0, e.st, a, e.origin, e.S, e.q[0]);
   const size_t lds_x = ((size_t)e.bin_nb + 4) * 4;
-  const size_t lds_a = bin_apply_lds_bytes(e.bin_BS);
+  const size_t lds_a = bin_apply_lds_words(e.bin_G, e.bin_BS) * 4;
   r = hipFuncSetAttribute((const void*)k_bin_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a);
   if (r != hipSuccess) return r;
   for (uint32_t d = 0; d < 254; ++d) {
+    if (a.qmin && (r = launch_bfs_level_step(e, record, d, 0, a.qmin)) != hipSuccess) return r;
     GS_ASZP_DISPATCH(e.ASZP, {
       r = hipFuncSetAttribute((const void*)k_bin_expand<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
       if (r != hipSuccess) return r;
       hipLaunchKernelGGL(k_bin_expand<A>, dim3(e.bin_G), dim3(BIN_THREADS), lds_x, e.st, a, d, e.q[d & 1]);
     });
-    hipLaunchKernelGGL(k_bin_apply, dim3(e.bin_nb), dim3(BIN_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
+    hipLaunchKernelGGL(k_bin_apply, dim3(e.bin_nb), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
     if ((d & 3) == 3) {  // poll the frontier size every 4 levels
       uint32_t* h = e.h_err + 1;
       if ((r = hipMemcpyAsync(h, e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st)) != hipSuccess) return r;

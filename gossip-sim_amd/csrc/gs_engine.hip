@@ -207,10 +207,10 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
     ALLOC(e->q[0], PAIRS, 0);
     ALLOC(e->q[1], PAIRS, 0);
   }
-  if (mode == GS_BFS_BINNED) {  // ~512 bins of 2^BS consecutive pairs, BS in [10, 15]
+  if (mode == GS_BFS_BINNED) {  // ~4096 bins of 2^BS consecutive pairs (L2-sized apply working set)
     uint32_t lg = 0;
     while ((1ull << lg) < PAIRS) ++lg;
-    e->bin_BS = std::min(15u, std::max(10u, lg > 9 ? lg - 9 : 0u));
+    e->bin_BS = std::min(14u, std::max(10u, lg > 12 ? lg - 12 : 0u));
     e->bin_nb = (uint32_t)((PAIRS + (1ull << e->bin_BS) - 1) >> e->bin_BS);
     e->bin_G = (uint32_t)std::min<size_t>(1024, std::max<size_t>(32, PAIRS / 2048));
     ALLOC(e->bin_pm, PAIRS, 0);

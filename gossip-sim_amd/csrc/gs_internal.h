@@ -126,6 +126,7 @@ hipError_t launch_scatter_rank(Engine& e, const uint32_t* sorted_ids, uint32_t* 
 hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket, uint32_t bits);
 hipError_t launch_bfs(Engine& e, bool record);
 hipError_t launch_bfs_binned(Engine& e, bool record);
+hipError_t launch_bfs_level_step(Engine& e, bool record, uint32_t d, uint32_t qmin, uint32_t qmax);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
 hipError_t launch_rotate(Engine& e, uint32_t round);
 hipError_t launch_stats(Engine& e, uint32_t rec_index, int mode);

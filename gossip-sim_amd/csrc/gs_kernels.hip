@@ -440,8 +440,9 @@ __global__ void k_bfs_seed(BfsArgs a, uint32_t* q0) {
 // Level-synchronous BFS over every slot at once (frontier of pair indices).
 template <int ASZP>
 __global__ __launch_bounds__(256) void k_bfs_level(BfsArgs a, uint32_t d, const uint32_t* __restrict__ qcur,
-                                                  uint32_t* __restrict__ qnxt) {
+                                                  uint32_t* __restrict__ qnxt, uint32_t qmin, uint32_t qmax) {
   const uint32_t qn = a.lvl[d];
+  if (qn < qmin || qn >= qmax) return;  // hybrid with the binned BFS: this level is the other kernel's
   const uint32_t N = a.N;
   bool overflow = false;
   for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < qn; i0 += gridDim.x * blockDim.x) {
@@ -464,6 +465,19 @@ __global__ __launch_bounds__(256) void k_bfs_level(BfsArgs a, uint32_t d, const 
     }
   }
   if (overflow) atomicOr(a.err, ERR_INBOUND);
+}
+
+static BfsArgs bfs_args(Engine& e);
+
+// One level of k_bfs_level, run only when qmin <= frontier size < qmax (the binned
+// BFS takes small levels this way: one atomic per push is cheap when there are few).
+hipError_t launch_bfs_level_step(Engine& e, bool record, uint32_t d, uint32_t qmin, uint32_t qmax) {
+  BfsArgs a = bfs_args(e);
+  a.record = record ? 1 : 0;
+  const uint32_t grid = (uint32_t)std::min<size_t>((qmax == 0xFFFFFFFFu ? e.PAIRS : qmax) / 256 + 1, 2048);
+  GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_bfs_level<A>, dim3(grid), dim3(256), 0, e.st, a, d, e.q[d & 1],
+                                              e.q[(d + 1) & 1], qmin, qmax));
+  return hipGetLastError();
 }
 
 static BfsArgs bfs_args(Engine& e) {
@@ -503,7 +517,7 @@ hipError_t launch_bfs(Engine& e, bool record) {
   const uint32_t grid = grid_for(e.PAIRS, 256, 2048);
   for (uint32_t d = 0; d < 254; ++d) {
     GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_bfs_level<A>, dim3(grid), dim3(256), 0, e.st, a, d, e.q[d & 1],
-                                                e.q[(d + 1) & 1]));
+                                                e.q[(d + 1) & 1], 0u, 0xFFFFFFFFu));
     if ((d & 3) == 3) {  // poll the frontier size every 4 levels
       uint32_t* h = e.h_err + 1;
       if ((r = hipMemcpyAsync(h, e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st)) != hipSuccess) return r;

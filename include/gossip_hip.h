@@ -52,7 +52,7 @@ enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24
  * propagation-blocked (pushes binned by destination range, LDS counters per
  * bin; large clusters). AUTO picks WORKGROUP, else BINNED, else LEVEL. */
 enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2, GS_BFS_BINNED = 3 };
-enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4 };
+enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4, GS_FLAG_BINNED_ALL_LEVELS = 8 };
 
 typedef struct gs_params {
   uint32_t push_fanout;         /* Config::gossip_push_fanout (gossip.rs:113) */
@@ -67,7 +67,9 @@ typedef struct gs_params {
                                    workgroup round (same results; for A/B measurement);
                                    GS_FLAG_NARROW_WAVE_PATH: the one-kernel round sends in-degrees
                                    > 24 (not > 64) to its ordered single-lane consume (same results;
-                                   lets small test clusters cover that path) */
+                                   lets small test clusters cover that path);
+                                   GS_FLAG_BINNED_ALL_LEVELS: GS_BFS_BINNED bins every level, not
+                                   only levels with >= 2^17 frontier pairs (same results) */
 } gs_params;
 
 typedef struct gs_slot {

@@ -20,6 +20,12 @@ U64MAX = np.uint64(2**64 - 1)
 MODES = [gs.GS_BFS_WORKGROUP, gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED]
 
 
+def ekw(mode):
+    """Engine kwargs of a BFS mode; small binned engines bin every level (else the
+    hybrid hands levels below 2^17 frontier pairs to the level kernel)."""
+    return dict(bfs_mode=mode, binned_all_levels=mode == gs.GS_BFS_BINNED)
+
+
 # ------------------------------------------------------------ reference KATs ----
 def six_node():
     d = json.load(open(os.path.join(HERE, "golden", "six_node_cluster.json")))
@@ -42,7 +48,7 @@ def upload_entries(eng, d, ids):
 def test_mst_kat_on_gpu(mode):
     """gossip.rs test_mst (1040-1163) through the HIP BFS."""
     d, ids, st = six_node()
-    eng = gs.Engine(st, 1, fanout=2, active_set_size=12, rotation_probability=0.2, seed=1, bfs_mode=mode)
+    eng = gs.Engine(st, 1, fanout=2, active_set_size=12, rotation_probability=0.2, seed=1, **ekw(mode))
     upload_entries(eng, d, ids)
     eng.set_slots([ids[5]])
     eng.run_gossip()
@@ -63,7 +69,7 @@ def test_mst_kat_on_gpu(mode):
 def test_pruning_kat_on_gpu(mode):
     """gossip_main.rs test_pruning (1071-1163): no prunes before iteration 19, then {3->M, M->h, j->P}."""
     d, ids, st = six_node()
-    eng = gs.Engine(st, 1, fanout=2, active_set_size=12, rotation_probability=0.2, seed=1, bfs_mode=mode)
+    eng = gs.Engine(st, 1, fanout=2, active_set_size=12, rotation_probability=0.2, seed=1, **ekw(mode))
     upload_entries(eng, d, ids)
     eng.set_slots([ids[5]], min_ingress=2, thresholds=0.15)
     inv = {v: k for k, v in enumerate(ids)}
@@ -85,7 +91,7 @@ def test_pruning_kat_on_gpu(mode):
 def make_pair(n, origin_ranks, *, asz=12, fanout=6, p=0.013333, seed=7, thr=0.15, mi=2, mode=gs.GS_BFS_AUTO):
     pks, st = eb.synth.network(n)
     S = len(origin_ranks)
-    eng = gs.Engine(st, S, fanout=fanout, active_set_size=asz, rotation_probability=p, seed=seed, bfs_mode=mode)
+    eng = gs.Engine(st, S, fanout=fanout, active_set_size=asz, rotation_probability=p, seed=seed, **ekw(mode))
     sims = [ob.Sim(ob.PHILOX, seed, pks, st, fanout) for _ in range(S)]
     origins = [sims[0].find_nth_largest(r) for r in origin_ranks]
     eng.set_slots(origins, mi, thr)
@@ -283,13 +289,16 @@ def test_large_network_invariants():
         assert (dest >= 0).all()
 
 
-def test_binned_bfs_matches_level_bfs_large():
-    """N = 300k, 3 slots, a fail-nodes fraction: the propagation-blocked BFS gives
-    the level BFS's hops, in-degrees, inbound sets, counters and summaries."""
+@pytest.mark.parametrize("all_levels", [False, True])
+def test_binned_bfs_matches_level_bfs_large(all_levels):
+    """N = 300k, 3 slots, a fail-nodes fraction: the propagation-blocked BFS (hybrid
+    with the level kernel for small levels, or binned throughout) gives the level
+    BFS's hops, in-degrees, inbound sets, counters and summaries."""
     n = 300_000
     st = eb.synth.power_law_stakes(n)
-    engs = [gs.Engine(st, 3, seed=33, rotation_probability=0.01, bfs_mode=m)
-            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED)]
+    engs = [gs.Engine(st, 3, seed=33, rotation_probability=0.01, bfs_mode=gs.GS_BFS_LEVEL),
+            gs.Engine(st, 3, seed=33, rotation_probability=0.01, bfs_mode=gs.GS_BFS_BINNED,
+                      binned_all_levels=all_levels)]
     for e in engs:
         e.set_slots([0, 17, n - 1], [2, 1, 3], [0.15, 0.3, 0.05])
         e.init_active_sets()
