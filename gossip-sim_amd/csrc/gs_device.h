@@ -17,6 +17,21 @@ constexpr uint32_t CACHE_LIMIT = 50; // ReceivedCacheEntry::CAPACITY
 constexpr uint32_t MIN_NUM_UPSERTS = 20;
 constexpr uint32_t PRUNED_FLAG = 0x80u;
 
+// A received-cache slot is one u32 word: node id (24 bits) | score (7 bits) << 24 |
+// pruned flag << 31. Key and score travel in one load and one store, so a score
+// increment is a plain store of a word the lookup already holds.
+constexpr uint32_t CK_ID = 0xFFFFFFu;
+__host__ __device__ inline uint32_t ck_id(uint32_t w) { return w & CK_ID; }
+__host__ __device__ inline uint32_t ck_score(uint32_t w) { return (w >> 24) & 0x7Fu; }
+__host__ __device__ inline bool ck_pruned(uint32_t w) { return (w >> 31) != 0; }
+// score_flag: score (<= 0x7F) | PRUNED_FLAG
+__host__ __device__ inline uint32_t ck_make(uint32_t id, uint32_t score_flag) { return id | (score_flag << 24); }
+// the slot with score + 1, saturating at 0x7F (received_cache.rs:88-90); clears the pruned flag
+__host__ __device__ inline uint32_t ck_bump(uint32_t w) {
+  const uint32_t s = ck_score(w);
+  return ck_make(ck_id(w), s < 0x7Fu ? s + 1 : 0x7Fu);
+}
+
 // Debug builds (make DEBUG_BOUNDS=1): every guarded index is checked; a violation
 // prints, raises ERR_BOUNDS and the access is skipped instead of faulting.
 constexpr uint32_t ERR_BOUNDS = 0x100u;

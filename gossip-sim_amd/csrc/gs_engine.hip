@@ -196,7 +196,6 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   ALLOC(e->inb, (size_t)e->capin * PAIRS, 0);
   ALLOC(e->cmeta, PAIRS, 0);
   ALLOC(e->ckey, (size_t)CACHE_CAP * PAIRS, 0);
-  ALLOC(e->cscore, (size_t)CACHE_CAP * PAIRS, 0);
   ALLOC(e->egress, PAIRS, 0);
   ALLOC(e->prune_round, PAIRS, 0);
   ALLOC(e->egress_acc, PAIRS, 0);
@@ -541,7 +540,8 @@ int gs_read_inbound(gs_engine* eh, uint32_t slot, uint32_t* off, uint32_t* src, 
   return GS_OK;
 }
 
-// Copies the cache columns of one slot: keys/scores [CACHE_CAP][N].
+// Copies the cache columns of one slot and splits the slot words (ck_make):
+// keys [CACHE_CAP][N] node ids, scores [CACHE_CAP][N] score | PRUNED_FLAG.
 static int read_cache_slot(Engine* e, uint32_t slot, std::vector<uint32_t>& meta, std::vector<uint32_t>& keys,
                            std::vector<uint8_t>& scores) {
   const size_t N = e->N, base = (size_t)slot * N;
@@ -549,8 +549,11 @@ static int read_cache_slot(Engine* e, uint32_t slot, std::vector<uint32_t>& meta
   HIPC(hipMemcpyAsync(meta.data(), e->cmeta + base, N * 4, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpy2DAsync(keys.data(), N * 4, e->ckey + base, e->PAIRS * 4, N * 4, CACHE_CAP, hipMemcpyDeviceToHost,
                         e->st));
-  HIPC(hipMemcpy2DAsync(scores.data(), N, e->cscore + base, e->PAIRS, N, CACHE_CAP, hipMemcpyDeviceToHost, e->st));
   HIPC(hipStreamSynchronize(e->st));
+  for (size_t i = 0; i < keys.size(); ++i) {
+    scores[i] = (uint8_t)(keys[i] >> 24);
+    keys[i] = ck_id(keys[i]);
+  }
   return GS_OK;
 }
 
@@ -584,25 +587,19 @@ int gs_read_cache(gs_engine* eh, uint32_t slot, uint32_t node, uint32_t* up, uin
   const size_t p = (size_t)slot * e->N + node;
   uint32_t meta = 0;
   uint32_t* dk = nullptr;
-  uint8_t* ds = nullptr;
   HIPC(hipMalloc(&dk, CACHE_CAP * 4));
-  HIPC(hipMalloc(&ds, CACHE_CAP));
   HIPC(hipMemcpyAsync(&meta, e->cmeta + p, 4, hipMemcpyDeviceToHost, e->st));
   HIPC(launch_gather_strided_u32(*e, e->ckey + p, e->PAIRS, CACHE_CAP, dk));
-  HIPC(launch_gather_strided_u8(*e, e->cscore + p, e->PAIRS, CACHE_CAP, ds));
   std::vector<uint32_t> k(CACHE_CAP);
-  std::vector<uint8_t> s(CACHE_CAP);
   HIPC(hipMemcpyAsync(k.data(), dk, CACHE_CAP * 4, hipMemcpyDeviceToHost, e->st));
-  HIPC(hipMemcpyAsync(s.data(), ds, CACHE_CAP, hipMemcpyDeviceToHost, e->st));
   HIPC(hipStreamSynchronize(e->st));
   hipFree(dk);
-  hipFree(ds);
   const uint32_t L = meta & 0xFF;
   *up = (meta >> 8) & 0xFF;
   *len = L;
   if (L > cap) return fail(GS_ERANGE, "cache buffer too small");
   std::vector<std::pair<uint32_t, uint32_t>> v;
-  for (uint32_t i = 0; i < L; ++i) v.push_back({k[i], (uint32_t)(s[i] & 0x7F)});
+  for (uint32_t i = 0; i < L; ++i) v.push_back({ck_id(k[i]), ck_score(k[i])});
   std::sort(v.begin(), v.end());
   for (uint32_t i = 0; i < L; ++i) { keys[i] = v[i].first; scores[i] = v[i].second; }
   return GS_OK;

@@ -58,8 +58,7 @@ struct Engine {
   uint32_t* mask = nullptr;
   uint32_t* inb = nullptr;
   uint32_t* cmeta = nullptr;
-  uint32_t* ckey = nullptr;
-  uint8_t* cscore = nullptr;
+  uint32_t* ckey = nullptr;  // received cache [CACHE_CAP][PAIRS] slot words: id | score << 24 | pruned << 31
   uint8_t* egress = nullptr;
   uint8_t* prune_round = nullptr;
   uint32_t* egress_acc = nullptr;
@@ -134,6 +133,5 @@ hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_index);
 size_t round_wg_lds_bytes(uint32_t N, uint32_t fcap, uint32_t ASZP);
 size_t bfs_wg_lds_bytes(uint32_t N);
 hipError_t launch_gather_strided_u32(Engine& e, const uint32_t* src, size_t stride, uint32_t n, uint32_t* dst);
-hipError_t launch_gather_strided_u8(Engine& e, const uint8_t* src, size_t stride, uint32_t n, uint8_t* dst);
 
 }  // namespace gs

@@ -541,8 +541,7 @@ struct CpArgs {
   const uint32_t* cnt;
   const uint32_t* inb;
   uint32_t* cmeta;
-  uint32_t* ckey;
-  uint8_t* cscore;
+  uint32_t* ckey;  // [CACHE_CAP][PAIRS] slot words (ck_make)
   uint8_t* prune_round;
   uint32_t* slot_prunes;
   uint32_t* mask;
@@ -599,22 +598,19 @@ __device__ inline void cp_generic(const CpArgs& a, size_t p, uint32_t o, uint32_
       if (k == 0) up = up < 255 ? up + 1 : 255;
       int found = -1;
       for (uint32_t i = 0; i < len; ++i)
-        if (a.ckey[(size_t)i * PAIRS + p] == src) { found = (int)i; break; }
+        if (ck_id(a.ckey[(size_t)i * PAIRS + p]) == src) { found = (int)i; break; }
       if (k < 2) {
         if (found >= 0) {
-          uint8_t& sc = a.cscore[(size_t)found * PAIRS + p];
-          const uint32_t s0 = sc & 0x7F;
-          sc = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
+          uint32_t& w = a.ckey[(size_t)found * PAIRS + p];
+          w = ck_bump(w);
         } else if (len < CACHE_CAP) {
-          a.ckey[(size_t)len * PAIRS + p] = src;
-          a.cscore[(size_t)len * PAIRS + p] = 1;
+          a.ckey[(size_t)len * PAIRS + p] = ck_make(src, 1u);
           ++len;
         } else {
           cache_overflow = true;
         }
       } else if (found < 0 && len < CACHE_LIMIT) {
-        a.ckey[(size_t)len * PAIRS + p] = src;
-        a.cscore[(size_t)len * PAIRS + p] = 0;
+        a.ckey[(size_t)len * PAIRS + p] = ck_make(src, 0u);
         ++len;
       }
     }
@@ -632,22 +628,22 @@ __device__ inline void cp_generic(const CpArgs& a, size_t p, uint32_t o, uint32_
       const uint64_t mis = min_ingress_stake(sv < so ? sv : so, a.thr[o]);
       const uint32_t mi = a.min_ingress[o];
       for (uint32_t i = 0; i < len; ++i) {
-        const uint32_t ki = a.ckey[(size_t)i * PAIRS + p];
-        const uint32_t si = a.cscore[(size_t)i * PAIRS + p] & 0x7F;
+        const uint32_t wi = a.ckey[(size_t)i * PAIRS + p];
+        const uint32_t ki = ck_id(wi), si = ck_score(wi);
         const uint64_t sti = a.stake[ki];
         uint32_t pos = 0;
         uint64_t cum = 0;
         for (uint32_t j = 0; j < len; ++j) {
           if (j == i) continue;
-          const uint32_t kj = a.ckey[(size_t)j * PAIRS + p];
-          const uint32_t sj = a.cscore[(size_t)j * PAIRS + p] & 0x7F;
+          const uint32_t wj = a.ckey[(size_t)j * PAIRS + p];
+          const uint32_t kj = ck_id(wj), sj = ck_score(wj);
           const uint64_t stj = a.stake[kj];
           // sort by Reverse((score, stake)); ties by ascending id (canonical order)
           const bool before = sj > si || (sj == si && (stj > sti || (stj == sti && kj < ki)));
           if (before) { ++pos; cum = sat_add(cum, stj); }
         }
         if (pos >= mi && cum >= mis && ki != org) {
-          a.cscore[(size_t)i * PAIRS + p] = (uint8_t)(si | PRUNED_FLAG);
+          a.ckey[(size_t)i * PAIRS + p] = ck_make(ki, si | PRUNED_FLAG);
           ++npr;
         }
       }
@@ -665,8 +661,9 @@ __device__ inline void cp_generic(const CpArgs& a, size_t p, uint32_t o, uint32_
   if (APPLY && plen) {
     const uint32_t org = a.origin[o], ob = a.obkt[o];
     for (uint32_t i = 0; i < plen; ++i) {
-      if (!(a.cscore[(size_t)i * PAIRS + p] & PRUNED_FLAG)) continue;
-      const uint32_t u = a.ckey[(size_t)i * PAIRS + p];
+      const uint32_t w = a.ckey[(size_t)i * PAIRS + p];
+      if (!ck_pruned(w)) continue;
+      const uint32_t u = ck_id(w);
       if (u != org) apply_prune(a, o, ob, u, v);
     }
   }
@@ -696,8 +693,9 @@ __device__ inline void cp_fast(const CpArgs& a, size_t p, uint32_t c, uint32_t m
     key[i] = 0xFFFFFFFFu;
     sc[i] = 0;
     if ((uint32_t)i < wlen) {
-      key[i] = (a.ckey + (size_t)i * PAIRS)[q];
-      sc[i] = (a.cscore + (size_t)i * PAIRS)[q];
+      const uint32_t w = (a.ckey + (size_t)i * PAIRS)[q];
+      key[i] = ck_id(w);
+      sc[i] = ck_score(w);
     }
   }
   asm volatile("" ::: "memory");  // keep the loads above: one wait for all of them
@@ -763,8 +761,7 @@ __device__ inline void cp_fast(const CpArgs& a, size_t p, uint32_t c, uint32_t m
 #pragma unroll
   for (int i = 0; i < FL; ++i)
     if ((dirty >> i) & 1u) {
-      (a.ckey + (size_t)i * PAIRS)[q] = key[i];
-      (a.cscore + (size_t)i * PAIRS)[q] = (uint8_t)sc[i];
+      (a.ckey + (size_t)i * PAIRS)[q] = ck_make(key[i], sc[i]);
     }
   a.cmeta[p] = len | (up << 8);
 }
@@ -832,7 +829,7 @@ hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply,
   CpArgs a;
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
   a.min_ingress = e.min_ingress; a.thr = e.thr; a.cnt = e.cnt; a.inb = e.inb; a.cmeta = e.cmeta; a.ckey = e.ckey;
-  a.cscore = e.cscore; a.prune_round = e.prune_round; a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.err = e.err;
+  a.prune_round = e.prune_round; a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.err = e.err;
   a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc; a.record = record ? 1 : 0;
   a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.ASZP = e.ASZP; a.capin = e.capin; a.PAIRS = e.PAIRS;
   const uint32_t grid = grid_for(e.PAIRS, 256, 8192);
@@ -1041,10 +1038,6 @@ __global__ void k_gather_strided(const T* __restrict__ src, size_t stride, uint3
 }
 hipError_t launch_gather_strided_u32(Engine& e, const uint32_t* src, size_t stride, uint32_t n, uint32_t* dst) {
   hipLaunchKernelGGL(k_gather_strided<uint32_t>, dim3(grid_for(n, 256)), dim3(256), 0, e.st, src, stride, n, dst);
-  return hipGetLastError();
-}
-hipError_t launch_gather_strided_u8(Engine& e, const uint8_t* src, size_t stride, uint32_t n, uint8_t* dst) {
-  hipLaunchKernelGGL(k_gather_strided<uint8_t>, dim3(grid_for(n, 256)), dim3(256), 0, e.st, src, stride, n, dst);
   return hipGetLastError();
 }
 

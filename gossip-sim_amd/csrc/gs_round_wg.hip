@@ -59,8 +59,7 @@ struct RoundArgs {
   uint32_t* cnt;
   uint32_t* mask;
   uint32_t* cmeta;
-  uint32_t* ckey;
-  uint8_t* cscore;
+  uint32_t* ckey;  // [CACHE_CAP][PAIRS] slot words (ck_make)
   uint8_t* egress;
   uint8_t* prune_round;
   uint32_t* egress_acc;
@@ -143,6 +142,16 @@ __device__ inline void apply_prune_r(const RoundArgs& a, size_t base, const uint
   }
 }
 
+// Bit j set when record j's id (low 16 bits of rk[j]) equals k, for j < NC (records
+// past the in-degree are 0xFFFFFFFF and their bits are never consulted).
+template <int NC>
+__device__ inline uint32_t match_ids(const uint32_t (&rk)[16], uint32_t k) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) m |= (uint32_t)((rk[j] & 0xFFFFu) == k) << j;
+  return m;
+}
+
 // ---- C: register path (1 <= c <= 16) ----
 __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t* recs, const uint8_t* hops_l,
                                     uint32_t c, uint32_t& len, uint32_t& up, uint32_t& errf) {
@@ -159,26 +168,27 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
       rk[j] = (uint32_t)j < c ? key : 0xFFFFFFFFu;
     }
   }
-  sort_net<16>(rk);
+  // records beyond wc are 0xFFFFFFFF already, so sorting the first 4/8/16 suffices
+  if (wc <= 4) sort_net<4>(rk);
+  else if (wc <= 8) sort_net<8>(rk);
+  else sort_net<16>(rk);
   // look the records up in the entry: rows streamed 8 at a time, loads issued together
-  uint32_t present = 0;
+  uint32_t present = 0, w0 = 0, w1 = 0;
   int idx0 = -1, idx1 = -1;
   const uint32_t wl = active_max<7>(len);
   for (uint32_t i0 = 0; i0 < wl; i0 += 8) {
     uint32_t kc[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) kc[t] = i0 + t < wl ? ntl(&(a.ckey + (size_t)(i0 + t) * PAIRS)[q]) : 0xFFFFFFFEu;
+    for (int t = 0; t < 8; ++t) kc[t] = i0 + t < wl ? ntl(&(a.ckey + (size_t)(i0 + t) * PAIRS)[q]) : 0u;
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const uint32_t i = i0 + t;
-      const uint32_t k = i < len ? kc[t] : 0xFFFFFFFEu;
-      uint32_t m = 0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) m |= (uint32_t)((rk[j] & 0xFFFFu) == k) << j;
+      const uint32_t k = i < len ? ck_id(kc[t]) : 0xFFFFFFFEu;  // never equals a u16 record id
+      const uint32_t m = wc <= 4 ? match_ids<4>(rk, k) : wc <= 8 ? match_ids<8>(rk, k) : match_ids<16>(rk, k);
       present |= m;
-      if (m & 1u) idx0 = (int)i;
-      if (m & 2u) idx1 = (int)i;
+      if (m & 1u) { idx0 = (int)i; w0 = kc[t]; }
+      if (m & 2u) { idx1 = (int)i; w1 = kc[t]; }
     }
   }
   up = up < 255 ? up + 1 : 255;  // rank 0 (received_cache.rs:84-86)
@@ -187,12 +197,9 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
     if ((uint32_t)j >= c) break;
     const int idx = j == 0 ? idx0 : idx1;
     if (idx >= 0) {
-      uint8_t* sp = a.cscore + (size_t)idx * PAIRS + p;
-      const uint32_t s0 = *sp & 0x7Fu;
-      *sp = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
+      nts(&(a.ckey + (size_t)idx * PAIRS)[q], ck_bump(j == 0 ? w0 : w1));
     } else if (len < CACHE_CAP) {
-      nts(&(a.ckey + (size_t)len * PAIRS)[q], rk[j] & 0xFFFFu);
-      nts(&(a.cscore + (size_t)len * PAIRS)[q], (uint8_t)1);
+      nts(&(a.ckey + (size_t)len * PAIRS)[q], ck_make(rk[j] & 0xFFFFu, 1u));
       ++len;
     } else {
       errf |= ERR_CACHE;
@@ -201,8 +208,7 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
 #pragma unroll
   for (int j = 2; j < 16; ++j) {  // rank order; inserted only while len < 50 (received_cache.rs:91-97)
     if ((uint32_t)j < c && !((present >> j) & 1u) && len < CACHE_LIMIT) {
-      nts(&(a.ckey + (size_t)len * PAIRS)[q], rk[j] & 0xFFFFu);
-      nts(&(a.cscore + (size_t)len * PAIRS)[q], (uint8_t)0);
+      nts(&(a.ckey + (size_t)len * PAIRS)[q], ck_make(rk[j] & 0xFFFFu, 0u));
       ++len;
     }
   }
@@ -217,22 +223,15 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, size_t base, const uin
   const uint32_t wl = active_max<6>(len);
   uint32_t sk[32];
   {
-    uint32_t kk[32], ss[32];
+    uint32_t kk[32];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      kk[i] = 0;
-      ss[i] = 0;
-      if ((uint32_t)i < wl) {
-        kk[i] = ntl(&(a.ckey + (size_t)i * PAIRS)[q]);
-        ss[i] = ntl(&(a.cscore + (size_t)i * PAIRS)[q]);
-      }
-    }
+    for (int i = 0; i < 32; ++i) kk[i] = (uint32_t)i < wl ? ntl(&(a.ckey + (size_t)i * PAIRS)[q]) : 0u;
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
       const bool in = (uint32_t)i < len;
-      const uint32_t pr = a.prank[in ? kk[i] : 0u];
-      sk[i] = in ? (((0x7Fu - (ss[i] & 0x7Fu)) << 24) | pr) : 0xFFFFFFFFu;
+      const uint32_t pr = a.prank[in ? ck_id(kk[i]) : 0u];
+      sk[i] = in ? (((0x7Fu - ck_score(kk[i])) << 24) | pr) : 0xFFFFFFFFu;
     }
   }
   if (wl <= 16) sort_net<16>(sk);
@@ -251,13 +250,12 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, size_t base, const uin
       if (tail && first == len) first = (uint32_t)i;
       const bool pruned = tail && node != org;
       npr += pruned;
-      nts(&(a.ckey + (size_t)i * PAIRS)[q], node);
-      nts(&(a.cscore + (size_t)i * PAIRS)[q], (uint8_t)((0x7Fu - (sk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u)));
+      nts(&(a.ckey + (size_t)i * PAIRS)[q], ck_make(node, (0x7Fu - (sk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u)));
       cum = sat_add(cum, st);
     }
   }
   for (uint32_t i = first; i < len; ++i) {  // prune_connections
-    const uint32_t u = (a.ckey + (size_t)i * PAIRS)[q];
+    const uint32_t u = ck_id((a.ckey + (size_t)i * PAIRS)[q]);
     if (u != org) apply_prune_r(a, base, nl_l, u, v);
   }
   return npr;
@@ -291,21 +289,18 @@ __device__ inline void consume_wave(const RoundArgs& a, size_t p, const uint16_t
   int found = -1;
   if (l < c)
     for (uint32_t i = 0; i < L0; ++i)
-      if (scr[i] == src) found = (int)i;
+      if (ck_id(scr[i]) == src) found = (int)i;
   const bool isnew = l < c && found < 0;
   const uint64_t nb = __ballot(isnew);
   const uint32_t n0 = (uint32_t)(nb & 1u), n1 = (uint32_t)((nb >> 1) & 1u);
   up = up < 255 ? up + 1 : 255;
   if (l < 2) {
     if (found >= 0) {
-      uint8_t* sp = a.cscore + (size_t)found * PAIRS + p;
-      const uint32_t s0 = *sp & 0x7Fu;
-      *sp = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
+      (a.ckey + (size_t)found * PAIRS)[q] = ck_bump(scr[found]);
     } else {
       const uint32_t pos = L0 + (l == 1 ? n0 : 0u);
       if (pos < CACHE_CAP) {
-        (a.ckey + (size_t)pos * PAIRS)[q] = src;
-        (a.cscore + (size_t)pos * PAIRS)[q] = 1;
+        (a.ckey + (size_t)pos * PAIRS)[q] = ck_make(src, 1u);
       } else {
         errf |= ERR_CACHE;
       }
@@ -315,10 +310,7 @@ __device__ inline void consume_wave(const RoundArgs& a, size_t p, const uint16_t
   const uint64_t rest = nb & ~3ull;
   if (l >= 2 && isnew) {
     const uint32_t pos = L1 + (uint32_t)__popcll(rest & ((1ull << l) - 1));
-    if (pos < CACHE_LIMIT) {
-      (a.ckey + (size_t)pos * PAIRS)[q] = src;
-      (a.cscore + (size_t)pos * PAIRS)[q] = 0;
-    }
+    if (pos < CACHE_LIMIT) (a.ckey + (size_t)pos * PAIRS)[q] = ck_make(src, 0u);
   }
   const uint32_t nrest = (uint32_t)__popcll(rest);
   len = L1 + (L1 < CACHE_LIMIT ? min(nrest, CACHE_LIMIT - L1) : 0u);
@@ -344,22 +336,19 @@ __device__ inline void consume_serial(const RoundArgs& a, size_t p, const uint16
       const uint32_t src = best & 0xFFFFu;
       int found = -1;
       for (uint32_t i = 0; i < ln; ++i)
-        if (a.ckey[(size_t)i * PAIRS + p] == src) { found = (int)i; break; }
+        if (ck_id(a.ckey[(size_t)i * PAIRS + p]) == src) { found = (int)i; break; }
       if (k < 2) {
         if (found >= 0) {
-          uint8_t* sp = a.cscore + (size_t)found * PAIRS + p;
-          const uint32_t s0 = *sp & 0x7Fu;
-          *sp = (uint8_t)(s0 < 0x7F ? s0 + 1 : 0x7F);
+          uint32_t* sp = a.ckey + (size_t)found * PAIRS + p;
+          *sp = ck_bump(*sp);
         } else if (ln < CACHE_CAP) {
-          a.ckey[(size_t)ln * PAIRS + p] = src;
-          a.cscore[(size_t)ln * PAIRS + p] = 1;
+          a.ckey[(size_t)ln * PAIRS + p] = ck_make(src, 1u);
           ++ln;
         } else {
           errf |= ERR_CACHE;
         }
       } else if (found < 0 && ln < CACHE_LIMIT) {
-        a.ckey[(size_t)ln * PAIRS + p] = src;
-        a.cscore[(size_t)ln * PAIRS + p] = 0;
+        a.ckey[(size_t)ln * PAIRS + p] = ck_make(src, 0u);
         ++ln;
       }
     }
@@ -382,9 +371,9 @@ __device__ inline uint32_t prune_wave(const RoundArgs& a, size_t base, const uin
     sk[t] = 0xFFFFFFFFu;
     nd[t] = 0;
     if (i < len) {
-      nd[t] = (a.ckey + (size_t)i * PAIRS)[q];
-      const uint32_t sc = (a.cscore + (size_t)i * PAIRS)[q] & 0x7Fu;
-      sk[t] = ((0x7Fu - sc) << 24) | a.prank[nd[t]];
+      const uint32_t w = (a.ckey + (size_t)i * PAIRS)[q];
+      nd[t] = ck_id(w);
+      sk[t] = ((0x7Fu - ck_score(w)) << 24) | a.prank[nd[t]];
     }
     scr[i] = sk[t];
   }
@@ -406,8 +395,7 @@ __device__ inline uint32_t prune_wave(const RoundArgs& a, size_t base, const uin
     bool pruned = false;
     if (i < len) {
       pruned = rank[t] >= mi && cum[t] >= mis && nd[t] != org;
-      (a.ckey + (size_t)rank[t] * PAIRS)[q] = nd[t];
-      (a.cscore + (size_t)rank[t] * PAIRS)[q] = (uint8_t)((0x7Fu - (sk[t] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
+      (a.ckey + (size_t)rank[t] * PAIRS)[q] = ck_make(nd[t], (0x7Fu - (sk[t] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
       if (pruned) apply_prune_r(a, base, nl_l, nd[t], v);
     }
     npr += (uint32_t)__popcll(__ballot(pruned));
@@ -564,6 +552,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
     if (d + 1 >= 255) { errf |= ERR_DEPTH; break; }
     unsigned long long tl0 = (a.phase_clk && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
     for (uint32_t i0 = 0; i0 < qn; i0 += RWG_THREADS) {
+      if (i0 + (wid << 6) >= qn) continue;  // wave-uniform: no frontier node for this wave
       const bool valid = i0 + tid < qn;
       uint32_t row[ASZP];
       uint32_t pushm = 0;
@@ -660,6 +649,10 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
       const uint32_t h = hops_l[v], c = cnt_l[v];
       const uint32_t pmv = h != 0xFF ? pm_l[v] : 0u;
       const uint32_t eg = __popc(pmv);
+      // the row load goes out before this node's stores and atomics: VMEM counts
+      // complete in order, so a load issued after them would wait for them too
+      uint32_t row[ASZP];
+      if (pmv) load_row<ASZP>(a.peers + (size_t)(v * NB + (nl_l[v] >> 11)) * ASZP, row);
       nts(&a.hops[p], (uint8_t)h);
       nts(&a.cnt[p], c);
       nts(&a.egress[p], (uint8_t)eg);
@@ -679,8 +672,6 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
         }
       }
       if (pmv) {
-        uint32_t row[ASZP];
-        load_row<ASZP>(a.peers + (size_t)(v * NB + (nl_l[v] >> 11)) * ASZP, row);
         uint32_t pos[ASZP];
         uint32_t* dummy = scr + lane;
 #pragma unroll
@@ -813,7 +804,7 @@ hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_slot) {
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.frank = e.frank; a.srank = e.srank;
   a.by_srank = e.by_srank; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake; a.origin = e.origin;
   a.obkt = e.obkt; a.nfail = e.nfail; a.min_ingress = e.min_ingress; a.thr = e.thr; a.slot_prunes = e.slot_prunes;
-  a.hops = e.hops; a.cnt = e.cnt; a.mask = e.mask; a.cmeta = e.cmeta; a.ckey = e.ckey; a.cscore = e.cscore;
+  a.hops = e.hops; a.cnt = e.cnt; a.mask = e.mask; a.cmeta = e.cmeta; a.ckey = e.ckey;
   a.egress = e.egress; a.prune_round = e.prune_round; a.egress_acc = e.egress_acc; a.ingress_acc = e.ingress_acc;
   a.prune_acc = e.prune_acc; a.strand = e.strand; a.hist_acc = e.hist_acc;
   a.sum = record ? e.sum + (size_t)rec_slot * e.S : nullptr;
