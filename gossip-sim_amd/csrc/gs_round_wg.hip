@@ -126,20 +126,23 @@ enum { C_QN = 0, C_NEXT = 1, C_ERR = 2, C_SEG = 3, C_VIS = 4, C_PUSH = 5, C_STR 
        C_NHC = 10, C_NHP = 11, C_KTH = 12, C_HCNT = 16, C_HSUM = 18, C_HMIN = 20, C_HMAX = 21, C_HMLO = 22,
        C_HMHI = 23 };
 
+// PushActiveSet::prune for one (prunee u, pruner v) pair (push_active_set.rs:56-71,143-151):
+// the bit of v's ring slot in u's entry for this slot's origin, if v is still there.
+// The row comes in with one set of loads and is matched in registers (a peer occurs
+// at most once in an entry, so at most one bit matches).
+template <int ASZP>
 __device__ inline void apply_prune_r(const RoundArgs& a, size_t base, const uint16_t* nl_l, uint32_t u, uint32_t v) {
-  // PushActiveSet::prune for one (prunee u, pruner v) pair (push_active_set.rs:56-71,143-151)
   const uint32_t nl = nl_l[u];
-  const uint32_t ent = u * NB + (nl >> 11);
   const uint32_t head = nl & 31u, L = (nl >> 5) & 63u;
-  const uint32_t* row = a.peers + (size_t)ent * ((a.ASZ + 3) & ~3u);
-  for (uint32_t j = 0; j < L; ++j) {
-    uint32_t slot = head + j;
-    if (slot >= a.ASZ) slot -= a.ASZ;
-    if (row[slot] == v) {
-      atomicOr(&a.mask[base + u], 1u << slot);
-      return;
-    }
+  uint32_t row[ASZP];
+  load_row<ASZP>(a.peers + (size_t)(u * NB + (nl >> 11)) * ASZP, row);
+  uint32_t hit = 0;
+#pragma unroll
+  for (int s = 0; s < ASZP; ++s) {
+    const uint32_t pos = (uint32_t)s >= head ? (uint32_t)s - head : (uint32_t)s + a.ASZ - head;
+    hit |= (uint32_t)((uint32_t)s < a.ASZ && pos < L && row[s] == v) << s;
   }
+  if (hit) atomicOr(&a.mask[base + u], hit);
 }
 
 // Bit j set when record j's id (low 16 bits of rk[j]) equals k, for j < NC (records
@@ -216,6 +219,7 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
 
 // ---- D: register path (len <= 32). Rows are rewritten in prune order with the
 // pruned flag; returns the number of prunees. ----
+template <int ASZP>
 __device__ inline uint32_t prune_lane(const RoundArgs& a, size_t base, const uint16_t* nl_l, uint32_t org, size_t p,
                                       uint32_t v, uint32_t len, uint32_t mi, uint64_t mis) {
   const size_t PAIRS = a.PAIRS;
@@ -227,36 +231,46 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, size_t base, const uin
 #pragma unroll
     for (int i = 0; i < 32; ++i) kk[i] = (uint32_t)i < wl ? ntl(&(a.ckey + (size_t)i * PAIRS)[q]) : 0u;
     asm volatile("" ::: "memory");
+    uint32_t pr[32];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const bool in = (uint32_t)i < len;
-      const uint32_t pr = a.prank[in ? ck_id(kk[i]) : 0u];
-      sk[i] = in ? (((0x7Fu - ck_score(kk[i])) << 24) | pr) : 0xFFFFFFFFu;
-    }
+    for (int i = 0; i < 32; ++i) pr[i] = (uint32_t)i < wl ? a.prank[(uint32_t)i < len ? ck_id(kk[i]) : 0u] : 0u;
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 32; ++i) sk[i] = (uint32_t)i < len ? (((0x7Fu - ck_score(kk[i])) << 24) | pr[i]) : 0xFFFFFFFFu;
   }
-  if (wl <= 16) sort_net<16>(sk);
+  if (wl <= 8) sort_net<8>(sk);
+  else if (wl <= 16) sort_net<16>(sk);
   else sort_net<32>(sk);
   // sorted_unstable_by_key(Reverse((score, stake))), ties by id; scan of pre-add
-  // cumulative stake; skip(min_ingress_nodes); skip_while(cum < min_ingress_stake)
+  // cumulative stake; skip(min_ingress_nodes); skip_while(cum < min_ingress_stake).
+  // Node ids and stakes of 8 sorted entries at a time are gathered with one wait.
   uint64_t cum = 0;
-  uint32_t first = len, npr = 0;
+  uint32_t npr = 0;
+  bool tail = false;
 #pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    if ((uint32_t)i < len) {
-      const uint32_t pr = sk[i] & 0xFFFFFFu;
-      const uint32_t node = a.by_prank[pr];
-      const uint64_t st = a.pstake[pr];
-      const bool tail = (uint32_t)i >= mi && cum >= mis;
-      if (tail && first == len) first = (uint32_t)i;
-      const bool pruned = tail && node != org;
-      npr += pruned;
-      nts(&(a.ckey + (size_t)i * PAIRS)[q], ck_make(node, (0x7Fu - (sk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u)));
-      cum = sat_add(cum, st);
+  for (int c0 = 0; c0 < 32; c0 += 8) {
+    if ((uint32_t)c0 >= wl) break;
+    uint32_t nd[8];
+    uint64_t st[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const uint32_t i = c0 + t, r = i < len ? sk[c0 + t] & 0xFFFFFFu : 0u;
+      nd[t] = a.by_prank[r];
+      st[t] = a.pstake[r];
     }
-  }
-  for (uint32_t i = first; i < len; ++i) {  // prune_connections
-    const uint32_t u = ck_id((a.ckey + (size_t)i * PAIRS)[q]);
-    if (u != org) apply_prune_r(a, base, nl_l, u, v);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const uint32_t i = c0 + t;
+      if (i < len) {
+        tail = tail || (i >= mi && cum >= mis);  // once past both skips, every later entry is pruned
+        const bool pruned = tail && nd[t] != org;
+        npr += pruned;
+        nts(&(a.ckey + (size_t)i * PAIRS)[q], ck_make(nd[t], (0x7Fu - (sk[c0 + t] >> 24)) | (pruned ? PRUNED_FLAG : 0u)));
+        if (pruned) apply_prune_r<ASZP>(a, base, nl_l, nd[t], v);  // prune_connections
+        cum = sat_add(cum, st[t]);
+      }
+    }
   }
   return npr;
 }
@@ -358,6 +372,7 @@ __device__ inline void consume_serial(const RoundArgs& a, size_t p, const uint16
 }
 
 // ---- D: wave path (any len <= 96), two entries per lane ----
+template <int ASZP>
 __device__ inline uint32_t prune_wave(const RoundArgs& a, size_t base, const uint16_t* nl_l, uint32_t org, size_t p,
                                       uint32_t v, uint32_t len, uint32_t mi, uint64_t mis, uint32_t* scr) {
   const size_t PAIRS = a.PAIRS;
@@ -396,7 +411,7 @@ __device__ inline uint32_t prune_wave(const RoundArgs& a, size_t base, const uin
     if (i < len) {
       pruned = rank[t] >= mi && cum[t] >= mis && nd[t] != org;
       (a.ckey + (size_t)rank[t] * PAIRS)[q] = ck_make(nd[t], (0x7Fu - (sk[t] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
-      if (pruned) apply_prune_r(a, base, nl_l, nd[t], v);
+      if (pruned) apply_prune_r<ASZP>(a, base, nl_l, nd[t], v);
     }
     npr += (uint32_t)__popcll(__ballot(pruned));
   }
@@ -718,7 +733,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
         continue;
       }
       const uint64_t sv = a.stake[v];
-      const uint32_t npr = prune_lane(a, base, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr));
+      const uint32_t npr = prune_lane<ASZP>(a, base, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr));
       npr_sum += npr;
       finish_node(a, p, meta, len, 0, npr, true);
     } else {
@@ -747,7 +762,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
       uint32_t npr = 0;
       if (due) {
         const uint64_t sv = a.stake[v];
-        npr = prune_wave(a, base, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr), scr);
+        npr = prune_wave<ASZP>(a, base, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr), scr);
         if (lane == 0) npr_sum += npr;
       }
       if (lane == 0) finish_node(a, p, meta, len, due ? 0u : up, npr, due);
