@@ -27,17 +27,26 @@ static int fail(int code, const std::string& msg) {
       return fail(GS_EHIP, std::string(#expr) + ": " + hipGetErrorString(_r));                  \
   } while (0)
 
+hipEvent_t Engine::ev_take() {
+  hipEvent_t x = nullptr;
+  if (!ev_pool.empty()) {
+    x = ev_pool.back();
+    ev_pool.pop_back();
+  } else {
+    hipEventCreate(&x);
+  }
+  return x;
+}
 void Engine::tbegin(const char* fam, hipEvent_t* a) {
   *a = nullptr;
   if (!(prm.flags & GS_FLAG_PROFILE)) return;
-  hipEventCreate(a);
+  *a = ev_take();
   hipEventRecord(*a, st);
   (void)fam;
 }
 void Engine::tend(const char* fam, hipEvent_t a) {
   if (!a) return;
-  hipEvent_t b;
-  hipEventCreate(&b);
+  hipEvent_t b = ev_take();
   hipEventRecord(b, st);
   timers[fam].ev.push_back({a, b});
 }
@@ -62,6 +71,8 @@ static int dalloc(Engine& e, T** p, size_t count, int fill = 0) {
     if (_s) { destroy_engine(e); return _s; }     \
   } while (0)
 
+static int flush_rot_clear(Engine* e);
+
 static void destroy_engine(Engine* e) {
   if (!e) return;
   if (e->st) hipStreamSynchronize(e->st);
@@ -69,6 +80,7 @@ static void destroy_engine(Engine* e) {
   if (e->h_err) hipHostFree(e->h_err);
   for (auto& kv : e->timers)
     for (auto& pr : kv.second.ev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+  for (hipEvent_t x : e->ev_pool) hipEventDestroy(x);
   if (e->st) hipStreamDestroy(e->st);
   delete e;
 }
@@ -218,7 +230,7 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   }
   ALLOC(e->lvl, 256, 0);
   ALLOC(e->rot_list, N, 0);
-  ALLOC(e->rot_count, 1, 0);
+  ALLOC(e->rot_count, 2, 0);
   ALLOC(e->rot_changed, N * NB, 0);
   ALLOC(e->work, PAIRS, 0);
   ALLOC(e->work_count, 1, 0);
@@ -228,7 +240,9 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   ALLOC(e->hist_acc, S * 256, 0);
   e->bm_words = (n + 31) / 32;
   ALLOC(e->bm, S * e->bm_words, 0);
-  e->sum_cap = 64;
+  // recorded-round summaries stay on the device until read back: a ring of up to
+  // 256 MiB (C2: ~1,400 rounds) so a measured run is never stalled by a drain
+  e->sum_cap = (uint32_t)std::max<size_t>(64, std::min<size_t>(4096, (256ull << 20) / (S * sizeof(gs_round_summary))));
   ALLOC(e->sum, (size_t)e->sum_cap * S, 0);
   ALLOC(e->err, 4, 0);
   if (const char* pp = std::getenv("GS_PHASE_PROFILE"); pp && pp[0] == '1') ALLOC(e->phase_clk, 16, 0);
@@ -294,6 +308,7 @@ static int reset_pair_state(Engine* e) {
 
 int gs_set_slots(gs_engine* eh, const gs_slot* slots, uint32_t n_slots) {
   ENGINE(eh);
+  if (int s_ = flush_rot_clear(e)) return s_;
   if (!slots || n_slots != e->S) return fail(GS_EINVAL, "gs_set_slots: need exactly n_slots entries");
   std::vector<uint32_t> org(e->S), mi(e->S);
   std::vector<uint8_t> ob(e->S);
@@ -329,6 +344,7 @@ int gs_sync(gs_engine* eh) {
 
 int gs_init_active_sets(gs_engine* eh) {
   ENGINE(eh);
+  if (int s_ = flush_rot_clear(e)) return s_;
   HIPC(launch_init_entries(*e));
   HIPC(hipMemsetAsync(e->mask, 0, e->PAIRS * 4, e->st));
   return GS_OK;
@@ -336,6 +352,7 @@ int gs_init_active_sets(gs_engine* eh) {
 
 int gs_set_active_set_entry(gs_engine* eh, uint32_t node, uint32_t bucket, const uint32_t* peers, uint32_t len) {
   ENGINE(eh);
+  if (int s_ = flush_rot_clear(e)) return s_;
   if (node >= e->N || bucket >= (uint32_t)NB) return fail(GS_EINVAL, "node/bucket out of range");
   if (len > e->ASZ) return fail(GS_ERANGE, "entry longer than active_set_size");
   std::vector<uint32_t> row(e->ASZP, 0);
@@ -408,6 +425,15 @@ static int need_slots(Engine* e) {
   return GS_OK;
 }
 
+// Applies a rotation's deferred prune-bit clear (left by the one-kernel gs_round)
+// before anything else reads or changes the prune masks.
+static int flush_rot_clear(Engine* e) {
+  if (!e->rot_clear_pending) return GS_OK;
+  e->rot_clear_pending = false;
+  HIPC(launch_rotate_clear(*e));
+  return GS_OK;
+}
+
 static int do_bfs(Engine* e, bool record) {
   hipEvent_t t0;
   e->tbegin("bfs", &t0);
@@ -422,10 +448,12 @@ static int do_bfs(Engine* e, bool record) {
 int gs_run_gossip(gs_engine* eh) {
   ENGINE(eh);
   if (int s = need_slots(e)) return s;
+  if (int s = flush_rot_clear(e)) return s;
   return do_bfs(e, false);
 }
 
 static int do_cp(Engine* e, bool c, bool p, bool a, bool record = false) {
+  if (int s = flush_rot_clear(e)) return s;
   hipEvent_t t0;
   e->tbegin("consume", &t0);
   hipError_t r = launch_consume_prune(*e, c, p, a, record);
@@ -441,9 +469,10 @@ int gs_chance_to_rotate(gs_engine* eh, uint32_t round) {
   ENGINE(eh);
   if (int s = need_slots(e)) return s;
   if (round >= (1u << 27)) return fail(GS_ERANGE, "round index must be < 2^27");
+  if (int s = flush_rot_clear(e)) return s;
   hipEvent_t t0;
   e->tbegin("rotate", &t0);
-  hipError_t r = launch_rotate(*e, round);
+  hipError_t r = launch_rotate(*e, round, false);
   e->tend("rotate", t0);
   HIPC(r);
   return GS_OK;
@@ -481,16 +510,23 @@ int gs_round(gs_engine* eh, uint32_t round, int record) {
   if (int s = need_slots(e)) return s;
   const bool rec = record != 0;
   if (e->fused) {  // BFS + consume + prune + statistics in one kernel per slot
+    if (round >= (1u << 27)) return fail(GS_ERANGE, "round index must be < 2^27");
     hipEvent_t t0;
     e->tbegin("round", &t0);
-    hipError_t r = launch_round_wg(*e, rec, e->sum_used);
+    const bool clr = e->rot_clear_pending;  // the last rotation's clear runs inside the round kernel
+    hipError_t r = launch_round_wg(*e, rec, e->sum_used, clr);
     e->tend("round", t0);
     HIPC(r);
+    e->rot_clear_pending = false;
     e->inb_valid = false;
-    if (int s = gs_chance_to_rotate(eh, round)) return s;
+    e->tbegin("rotate", &t0);
+    r = launch_rotate(*e, round, true);
+    e->tend("rotate", t0);
+    HIPC(r);
     if (rec && ++e->sum_used == e->sum_cap) return drain_summaries(e);
     return GS_OK;
   }
+  if (int s = flush_rot_clear(e)) return s;
   if (int s = do_bfs(e, rec)) return s;
   if (int s = do_cp(e, true, true, true, rec)) return s;
   if (int s = gs_chance_to_rotate(eh, round)) return s;
@@ -607,6 +643,7 @@ int gs_read_cache(gs_engine* eh, uint32_t slot, uint32_t node, uint32_t* up, uin
 
 int gs_read_pruned(gs_engine* eh, uint32_t slot, uint32_t node, uint32_t* fifo_mask) {
   ENGINE(eh);
+  if (int s_ = flush_rot_clear(e)) return s_;
   SLOT_CHECK(slot);
   if (node >= e->N) return fail(GS_EINVAL, "node out of range");
   if (int s = check_err(e)) return s;
@@ -671,6 +708,7 @@ int gs_read_caches(gs_engine* eh, uint32_t slot, uint32_t* up, uint32_t* len, ui
 
 int gs_read_pruned_all(gs_engine* eh, uint32_t slot, uint32_t* fifo_mask) {
   ENGINE(eh);
+  if (int s_ = flush_rot_clear(e)) return s_;
   SLOT_CHECK(slot);
   if (int s = check_err(e)) return s;
   const size_t N = e->N;
@@ -778,8 +816,8 @@ int gs_kernel_time(gs_engine* eh, const char* family, double* ms, uint64_t* laun
     hipEventElapsedTime(&x, pr.first, pr.second);
     t.ms += x;
     t.n += 1;
-    hipEventDestroy(pr.first);
-    hipEventDestroy(pr.second);
+    e->ev_pool.push_back(pr.first);
+    e->ev_pool.push_back(pr.second);
   }
   t.ev.clear();
   *ms = t.ms;
@@ -791,7 +829,7 @@ int gs_kernel_time_reset(gs_engine* eh) {
   ENGINE(eh);
   HIPC(hipStreamSynchronize(e->st));
   for (auto& kv : e->timers) {
-    for (auto& pr : kv.second.ev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+    for (auto& pr : kv.second.ev) { e->ev_pool.push_back(pr.first); e->ev_pool.push_back(pr.second); }
     kv.second.ev.clear();
     kv.second.ms = 0;
     kv.second.n = 0;

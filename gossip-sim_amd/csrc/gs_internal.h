@@ -75,8 +75,12 @@ struct Engine {
   uint32_t bin_G = 0, bin_BS = 0, bin_nb = 0;
   // rotation
   uint32_t* rot_list = nullptr;
-  uint32_t* rot_count = nullptr;
-  uint32_t* rot_changed = nullptr;
+  uint32_t* rot_count = nullptr;    // [2]: rotation r counts into [r & 1] and zeroes [(r + 1) & 1]
+  uint32_t* rot_changed = nullptr;  // [N][25] replaced ring slots of the last rotation, per entry
+  bool rot_clear_pending = false;   // the last rotation's prune-bit clear is still to be applied
+  bool rot_have_prev = false;
+  uint32_t rot_parity = 0;          // parity of the last rotation's round
+  size_t rwg_attr_lds = 0;          // dynamic LDS the round kernel was last configured for
   // fused consume -> prune worklist
   uint32_t* work = nullptr;
   uint32_t* work_count = nullptr;
@@ -100,6 +104,8 @@ struct Engine {
   // profiling
   struct Timed { std::vector<std::pair<hipEvent_t, hipEvent_t>> ev; double ms = 0; uint64_t n = 0; };
   std::map<std::string, Timed> timers;
+  std::vector<hipEvent_t> ev_pool;  // recycled events: no hipEventCreate per launch
+  hipEvent_t ev_take();
   void tbegin(const char* fam, hipEvent_t* a);
   void tend(const char* fam, hipEvent_t a);
 };
@@ -127,9 +133,13 @@ hipError_t launch_bfs(Engine& e, bool record);
 hipError_t launch_bfs_binned(Engine& e, bool record);
 hipError_t launch_bfs_level_step(Engine& e, bool record, uint32_t d, uint32_t qmin, uint32_t qmax);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
-hipError_t launch_rotate(Engine& e, uint32_t round);
+// Rotation of round `round` (decide + entries); the prune-bit clear of the replaced
+// ring slots runs now, or with defer_clear it is left pending for the next one-kernel
+// round (which applies it to its LDS copy of the masks) or launch_rotate_clear.
+hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear);
+hipError_t launch_rotate_clear(Engine& e);
 hipError_t launch_stats(Engine& e, uint32_t rec_index, int mode);
-hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_index);
+hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_index, bool rot_clear);
 size_t round_wg_lds_bytes(uint32_t N, uint32_t fcap, uint32_t ASZP);
 size_t bfs_wg_lds_bytes(uint32_t N);
 hipError_t launch_gather_strided_u32(Engine& e, const uint32_t* src, size_t stride, uint32_t n, uint32_t* dst);

@@ -136,8 +136,9 @@ hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket_k, 
 
 // ---------------------------------------------------------- rotation (R14) ----
 __global__ void k_rotate_decide(uint32_t N, uint64_t seed, uint32_t round, double p, uint32_t* rot_list,
-                                uint32_t* rot_count) {
+                                uint32_t* rot_count, uint32_t* rot_count_other) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u == 0) *rot_count_other = 0;  // the next rotation's counter (its last reader ran before this kernel)
   if (u >= N) return;
   Philox s(seed, P_DECIDE, u, round);
   if (unit_f64(s.next()) < p) rot_list[atomicAdd(rot_count, 1u)] = u;
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(256) void k_rotate_entries(const uint8_t* __restric
       break;
     }
     hl[ent] = (uint16_t)((L << 8) | head);
-    rot_changed[gid] = changed;
+    rot_changed[ent] = changed;
   }
 }
 
@@ -214,22 +215,35 @@ __global__ void k_rotate_clear(uint32_t N, uint32_t S, const uint8_t* __restrict
     const uint32_t i = gid / S, o = gid - i * S;
     const uint32_t u = rot_list[i];
     const uint32_t b = min((uint32_t)bucket[u], (uint32_t)obkt[o]);
-    const uint32_t m = rot_changed[i * NB + b];
+    const uint32_t m = rot_changed[u * NB + b];
     if (m) mask[(size_t)o * N + u] &= ~m;
   }
 }
 
-hipError_t launch_rotate(Engine& e, uint32_t round) {
-  hipError_t r = hipMemsetAsync(e.rot_count, 0, sizeof(uint32_t), e.st);
-  if (r != hipSuccess) return r;
-  hipLaunchKernelGGL(k_rotate_decide, dim3(grid_for(e.N, 256)), dim3(256), 0, e.st, e.N, e.prm.seed, round,
-                     e.prm.rotation_probability, e.rot_list, e.rot_count);
-  GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_rotate_entries<A>, dim3(grid_for((size_t)e.N * NB, 256, 2048)),
-                                              dim3(256), 0, e.st, e.bucket, e.P, e.peers, e.hl, e.rot_list,
-                                              e.rot_count, e.rot_changed, e.N, e.ASZ, e.prm.seed, round));
+hipError_t launch_rotate_clear(Engine& e) {
   hipLaunchKernelGGL(k_rotate_clear, dim3(grid_for((size_t)e.N * e.S, 256, 2048)), dim3(256), 0, e.st, e.N, e.S,
-                     e.bucket, e.obkt, e.rot_list, e.rot_count, e.rot_changed, e.mask);
+                     e.bucket, e.obkt, e.rot_list, e.rot_count + e.rot_parity, e.rot_changed, e.mask);
   return hipGetLastError();
+}
+
+hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear) {
+  const uint32_t par = round & 1u;
+  uint32_t* cnt = e.rot_count + par;
+  if (e.rot_have_prev && par == e.rot_parity) {  // rounds not consecutive: this counter was not pre-zeroed
+    hipError_t r = hipMemsetAsync(cnt, 0, sizeof(uint32_t), e.st);
+    if (r != hipSuccess) return r;
+  }
+  hipLaunchKernelGGL(k_rotate_decide, dim3(grid_for(e.N, 256)), dim3(256), 0, e.st, e.N, e.prm.seed, round,
+                     e.prm.rotation_probability, e.rot_list, cnt, e.rot_count + (par ^ 1u));
+  GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_rotate_entries<A>, dim3(grid_for((size_t)e.N * NB, 256, 2048)),
+                                              dim3(256), 0, e.st, e.bucket, e.P, e.peers, e.hl, e.rot_list, cnt,
+                                              e.rot_changed, e.N, e.ASZ, e.prm.seed, round));
+  e.rot_parity = par;
+  e.rot_have_prev = true;
+  e.rot_clear_pending = true;
+  if (defer_clear) return hipGetLastError();
+  e.rot_clear_pending = false;
+  return launch_rotate_clear(e);
 }
 
 // ------------------------------------------------------------- BFS (R8) ----

@@ -29,14 +29,21 @@
 
 namespace gs {
 
-#ifndef RWG_MIN_WAVES
-#define RWG_MIN_WAVES 4  // waves per SIMD (VGPR budget 128); LDS allows 2 workgroups per CU at C2
+#ifndef RWG_THREADS_N
+#define RWG_THREADS_N 768  // 12 waves: 2 workgroups per CU (LDS) = 6 waves per SIMD (VGPR budget 80)
 #endif
-constexpr uint32_t RWG_THREADS = 512;
+#ifndef RWG_MIN_WAVES
+#define RWG_MIN_WAVES (RWG_THREADS_N / 128)  // waves per SIMD at 2 workgroups per CU (the LDS limit at C2)
+#endif
+#ifndef GS_NT_STORES
+#define GS_NT_STORES 1
+#endif
+constexpr uint32_t RWG_THREADS = RWG_THREADS_N;
 constexpr uint32_t RWG_WAVES = RWG_THREADS / 64;
 constexpr uint32_t RWG_SCR = 128;  // per-wave LDS scratch (u32): staged cache keys / prune keys
 constexpr uint32_t LANE_C = 16;    // register path: in-degree <= 16
-constexpr uint32_t LANE_L = 32;    // register prune path: cache entry <= 32 keys
+constexpr int LANE_L = 16;         // register prune path: cache entry <= 16 keys (the wave path
+                                   // takes longer entries; at prune time they are rare)
 
 struct RoundArgs {
   const uint64_t* stake;
@@ -68,6 +75,11 @@ struct RoundArgs {
   uint32_t* strand;
   uint64_t* hist_acc;
   gs_round_summary* sum;  // this round's row [S] of the summary ring (record only)
+  // the last rotation's pending prune-bit clear (null when none): replaced ring slots
+  // of rotated node u's entry k are rot_changed[u * 25 + k]
+  const uint32_t* rot_list;
+  const uint32_t* rot_count;
+  const uint32_t* rot_changed;
   uint32_t* err;
   unsigned long long* phase_clk;  // optional: per-phase clock sums (thread 0 of each workgroup)
   uint32_t wave_c_max;            // in-degree bound of the wave consume path (64; 24 for path coverage)
@@ -88,19 +100,23 @@ struct RoundArgs {
 
 // LDS carve-up (byte offsets), shared by the host's size query and the kernel.
 struct RwgLayout {
-  uint32_t ctrl, hist, scr, cnt, qo, pm, mk, nl, hops, bm, rec, total;
+  uint32_t ctrl, hist, scr, cnt, qo, pm, mk, eg, nl, hops, bm, rec, total;
 };
-// pmw: bytes per push mask (2 when the ring has <= 16 slots)
-__host__ __device__ inline RwgLayout rwg_layout(uint32_t N, uint32_t fcap, uint32_t pmw) {
+// pmw: bytes per push mask (2 when the ring has <= 16 slots); offw: bytes per segment
+// offset (2 when every round's inbound records, <= fcap * N, fit in a u16 index)
+__host__ __device__ inline RwgLayout rwg_layout(uint32_t N, uint32_t fcap, uint32_t pmw, uint32_t offw) {
   RwgLayout L;
   uint32_t o = 0;
   L.ctrl = o; o += 32 * 4;
   L.hist = o; o += 256 * 4;
   L.scr = o;  o += RWG_WAVES * RWG_SCR * 4;
   L.cnt = o;  o += 4 * ((N + 1) / 2);           // in-degree u16 (atomics on the containing u32)
-  L.qo = o;   o += 4 * N;                       // BFS queues 2 x u16[N], then segment ends u32[N]
+  L.qo = o;   o += (offw * N + 3) & ~3u;        // the BFS queue u16[N] (each node enters once, levels
+                                                //   are consecutive ranges), then segment ends
   L.pm = o;   o += (pmw * N + 3) & ~3u;         // push masks, then the heavy-node list u16[N]
-  L.mk = o;   o += (pmw * N + 3) & ~3u;         // the slot's prune masks, staged for the BFS
+  L.mk = o;   o += (pmw * N + 3) & ~3u;         // the slot's prune masks: staged for the BFS, prunes
+                                                //   applied here, written back after a prune round
+  L.eg = o;   o += (N + 3) & ~3u;               // egress per node (popcount of the push mask)
   L.nl = o;   o += (2 * N + 3) & ~3u;           // per node: ring head | len << 5 | entry bucket << 11
   L.hops = o; o += (N + 3) & ~3u;
   L.bm = o;   o += ((N + 31) / 32) * 4;         // stranded bitmap over stake rank
@@ -109,8 +125,10 @@ __host__ __device__ inline RwgLayout rwg_layout(uint32_t N, uint32_t fcap, uint3
   return L;
 }
 
+__host__ __device__ inline bool rwg_off16(uint32_t N, uint32_t fcap) { return (uint64_t)fcap * N <= 0xFFFFu; }
+
 size_t round_wg_lds_bytes(uint32_t N, uint32_t fcap, uint32_t ASZP) {
-  return rwg_layout(N, fcap, ASZP <= 16 ? 2 : 4).total;
+  return rwg_layout(N, fcap, ASZP <= 16 ? 2 : 4, rwg_off16(N, fcap) ? 2 : 4).total;
 }
 
 // Streaming per-pair state (read or written once per round, ~0.5 GB/round at C2)
@@ -119,19 +137,26 @@ size_t round_wg_lds_bytes(uint32_t N, uint32_t fcap, uint32_t ASZP) {
 template <class T>
 __device__ inline T ntl(const T* p) { return __builtin_nontemporal_load(p); }
 template <class T>
-__device__ inline void nts(T* p, T v) { __builtin_nontemporal_store(v, p); }
+__device__ inline void nts(T* p, T v) {
+#if GS_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 
 // ctrl words
 enum { C_QN = 0, C_NEXT = 1, C_ERR = 2, C_SEG = 3, C_VIS = 4, C_PUSH = 5, C_STR = 6, C_PRUNES = 7, C_SSUM = 8,
        C_NHC = 10, C_NHP = 11, C_KTH = 12, C_HCNT = 16, C_HSUM = 18, C_HMIN = 20, C_HMAX = 21, C_HMLO = 22,
-       C_HMHI = 23 };
+       C_HMHI = 23, C_LVL = 25 /* 25..27: BFS level sizes, rotating by level mod 3 */, C_MDIRTY = 28 };
 
 // PushActiveSet::prune for one (prunee u, pruner v) pair (push_active_set.rs:56-71,143-151):
 // the bit of v's ring slot in u's entry for this slot's origin, if v is still there.
 // The row comes in with one set of loads and is matched in registers (a peer occurs
-// at most once in an entry, so at most one bit matches).
+// at most once in an entry, so at most one bit matches). The bit goes into the
+// slot's LDS copy of the masks (mkw: u16 per node when the ring has <= 16 slots).
 template <int ASZP>
-__device__ inline void apply_prune_r(const RoundArgs& a, size_t base, const uint16_t* nl_l, uint32_t u, uint32_t v) {
+__device__ inline void apply_prune_r(const RoundArgs& a, uint32_t* mkw, const uint16_t* nl_l, uint32_t u, uint32_t v) {
   const uint32_t nl = nl_l[u];
   const uint32_t head = nl & 31u, L = (nl >> 5) & 63u;
   uint32_t row[ASZP];
@@ -142,7 +167,22 @@ __device__ inline void apply_prune_r(const RoundArgs& a, size_t base, const uint
     const uint32_t pos = (uint32_t)s >= head ? (uint32_t)s - head : (uint32_t)s + a.ASZ - head;
     hit |= (uint32_t)((uint32_t)s < a.ASZ && pos < L && row[s] == v) << s;
   }
-  if (hit) atomicOr(&a.mask[base + u], hit);
+  if (hit) {
+    if (ASZP <= 16) atomicOr(&mkw[u >> 1], hit << ((u & 1u) << 4));
+    else atomicOr(&mkw[u], hit);
+  }
+}
+
+// Segment cursor fetch-and-increment (pu) or a dummy LDS atomic (so every slot of
+// the row issues one atomic and the wait comes once). u16 cursors share a u32 word;
+// their values stay below 2^16, so the add never carries into the neighbour.
+template <bool OFF16>
+__device__ inline uint32_t off_fetch_inc(uint32_t* offw, uint32_t w, bool pu, uint32_t* dummy) {
+  if (OFF16) {
+    const uint32_t sh = (w & 1u) << 4;
+    return (atomicAdd(pu ? &offw[w >> 1] : dummy, pu ? 1u << sh : 0u) >> sh) & 0xFFFFu;
+  }
+  return atomicAdd(pu ? &offw[w] : dummy, pu ? 1u : 0u);
 }
 
 // Bit j set when record j's id (low 16 bits of rk[j]) equals k, for j < NC (records
@@ -220,27 +260,26 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
 // ---- D: register path (len <= 32). Rows are rewritten in prune order with the
 // pruned flag; returns the number of prunees. ----
 template <int ASZP>
-__device__ inline uint32_t prune_lane(const RoundArgs& a, size_t base, const uint16_t* nl_l, uint32_t org, size_t p,
+__device__ inline uint32_t prune_lane(const RoundArgs& a, uint32_t* mkw, const uint16_t* nl_l, uint32_t org, size_t p,
                                       uint32_t v, uint32_t len, uint32_t mi, uint64_t mis) {
   const size_t PAIRS = a.PAIRS;
   const uint32_t q = (uint32_t)p;
-  const uint32_t wl = active_max<6>(len);
-  uint32_t sk[32];
+  const uint32_t wl = active_max<5>(len);
+  uint32_t sk[LANE_L];
   {
-    uint32_t kk[32];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) kk[i] = (uint32_t)i < wl ? ntl(&(a.ckey + (size_t)i * PAIRS)[q]) : 0u;
+    for (int i = 0; i < LANE_L; ++i) sk[i] = (uint32_t)i < wl ? ntl(&(a.ckey + (size_t)i * PAIRS)[q]) : 0u;
     asm volatile("" ::: "memory");
-    uint32_t pr[32];
+    uint32_t pr[LANE_L];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) pr[i] = (uint32_t)i < wl ? a.prank[(uint32_t)i < len ? ck_id(kk[i]) : 0u] : 0u;
+    for (int i = 0; i < LANE_L; ++i) pr[i] = (uint32_t)i < wl ? a.prank[(uint32_t)i < len ? ck_id(sk[i]) : 0u] : 0u;
     asm volatile("" ::: "memory");
 #pragma unroll
-    for (int i = 0; i < 32; ++i) sk[i] = (uint32_t)i < len ? (((0x7Fu - ck_score(kk[i])) << 24) | pr[i]) : 0xFFFFFFFFu;
+    for (int i = 0; i < LANE_L; ++i)
+      sk[i] = (uint32_t)i < len ? (((0x7Fu - ck_score(sk[i])) << 24) | pr[i]) : 0xFFFFFFFFu;
   }
   if (wl <= 8) sort_net<8>(sk);
-  else if (wl <= 16) sort_net<16>(sk);
-  else sort_net<32>(sk);
+  else sort_net<LANE_L>(sk);
   // sorted_unstable_by_key(Reverse((score, stake))), ties by id; scan of pre-add
   // cumulative stake; skip(min_ingress_nodes); skip_while(cum < min_ingress_stake).
   // Node ids and stakes of 8 sorted entries at a time are gathered with one wait.
@@ -248,7 +287,7 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, size_t base, const uin
   uint32_t npr = 0;
   bool tail = false;
 #pragma unroll
-  for (int c0 = 0; c0 < 32; c0 += 8) {
+  for (int c0 = 0; c0 < LANE_L; c0 += 8) {
     if ((uint32_t)c0 >= wl) break;
     uint32_t nd[8];
     uint64_t st[8];
@@ -267,7 +306,7 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, size_t base, const uin
         const bool pruned = tail && nd[t] != org;
         npr += pruned;
         nts(&(a.ckey + (size_t)i * PAIRS)[q], ck_make(nd[t], (0x7Fu - (sk[c0 + t] >> 24)) | (pruned ? PRUNED_FLAG : 0u)));
-        if (pruned) apply_prune_r<ASZP>(a, base, nl_l, nd[t], v);  // prune_connections
+        if (pruned) apply_prune_r<ASZP>(a, mkw, nl_l, nd[t], v);  // prune_connections
         cum = sat_add(cum, st[t]);
       }
     }
@@ -373,7 +412,7 @@ __device__ inline void consume_serial(const RoundArgs& a, size_t p, const uint16
 
 // ---- D: wave path (any len <= 96), two entries per lane ----
 template <int ASZP>
-__device__ inline uint32_t prune_wave(const RoundArgs& a, size_t base, const uint16_t* nl_l, uint32_t org, size_t p,
+__device__ inline uint32_t prune_wave(const RoundArgs& a, uint32_t* mkw, const uint16_t* nl_l, uint32_t org, size_t p,
                                       uint32_t v, uint32_t len, uint32_t mi, uint64_t mis, uint32_t* scr) {
   const size_t PAIRS = a.PAIRS;
   const uint32_t q = (uint32_t)p;
@@ -411,7 +450,7 @@ __device__ inline uint32_t prune_wave(const RoundArgs& a, size_t base, const uin
     if (i < len) {
       pruned = rank[t] >= mi && cum[t] >= mis && nd[t] != org;
       (a.ckey + (size_t)rank[t] * PAIRS)[q] = ck_make(nd[t], (0x7Fu - (sk[t] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
-      if (pruned) apply_prune_r<ASZP>(a, base, nl_l, nd[t], v);
+      if (pruned) apply_prune_r<ASZP>(a, mkw, nl_l, nd[t], v);
     }
     npr += (uint32_t)__popcll(__ballot(pruned));
   }
@@ -509,24 +548,26 @@ __device__ inline void wave_hop_stats(const uint32_t* hist, uint32_t* ctrl) {
   }
 }
 
-template <int ASZP>
+template <int ASZP, bool OFF16>
 __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundArgs a) {
   using PMT = typename std::conditional<(ASZP <= 16), uint16_t, uint32_t>::type;
+  using OFFT = typename std::conditional<OFF16, uint16_t, uint32_t>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t N = a.N;
-  const RwgLayout L = rwg_layout(N, a.fcap, (uint32_t)sizeof(PMT));
+  const RwgLayout L = rwg_layout(N, a.fcap, (uint32_t)sizeof(PMT), (uint32_t)sizeof(OFFT));
   uint32_t* ctrl = reinterpret_cast<uint32_t*>(smem + L.ctrl);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem + L.hist);
   uint32_t* cntw = reinterpret_cast<uint32_t*>(smem + L.cnt);
   const uint16_t* cnt_l = reinterpret_cast<const uint16_t*>(smem + L.cnt);
   uint16_t* q0 = reinterpret_cast<uint16_t*>(smem + L.qo);
-  uint16_t* q1 = q0 + N;
-  uint32_t* off_l = reinterpret_cast<uint32_t*>(smem + L.qo);
+  OFFT* off_l = reinterpret_cast<OFFT*>(smem + L.qo);
+  uint32_t* offw = reinterpret_cast<uint32_t*>(smem + L.qo);
   PMT* pm_l = reinterpret_cast<PMT*>(smem + L.pm);
   uint16_t* hv_l = reinterpret_cast<uint16_t*>(smem + L.pm);  // heavy nodes: consume from the front,
                                                               // prune-only from the back
   uint16_t* nl_l = reinterpret_cast<uint16_t*>(smem + L.nl);
   PMT* mk_l = reinterpret_cast<PMT*>(smem + L.mk);
+  uint32_t* mkw = reinterpret_cast<uint32_t*>(smem + L.mk);
   uint8_t* hops_l = smem + L.hops;
   uint32_t* bm_l = reinterpret_cast<uint32_t*>(smem + L.bm);
   uint16_t* rec_l = reinterpret_cast<uint16_t*>(smem + L.rec);
@@ -553,18 +594,36 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   for (uint32_t i = tid; i < W; i += RWG_THREADS) bm_l[i] = 0;
   if (tid < 32) ctrl[tid] = 0;
   __syncthreads();
-  if (tid == 0) { ctrl[C_QN] = 1; hops_l[org] = 0; q0[0] = (uint16_t)org; }
+  if (a.rot_count) {  // Cluster::chance_to_rotate's fresh filters (gossip.rs:739-754): the replaced
+                      // ring slots of the last rotation lose this slot's prune bits
+    const uint32_t nr = *a.rot_count;
+    for (uint32_t i = tid; i < nr; i += RWG_THREADS) {
+      const uint32_t u = a.rot_list[i];
+      const uint32_t m = a.rot_changed[u * NB + min((uint32_t)a.bucket[u], ob)];
+      if (m && (mk_l[u] & m)) {
+        mk_l[u] = (PMT)(mk_l[u] & ~m);
+        ctrl[C_MDIRTY] = 1;
+      }
+    }
+  }
+  if (tid == 0) { ctrl[C_LVL] = 1; hops_l[org] = 0; q0[0] = (uint16_t)org; }
   __syncthreads();
   RWG_MARK(0);
 
   // ---------------- A: BFS -------------------------------------------------
   unsigned long long prof[5] = {0, 0, 0, 0, 0};  // profiling builds of the run only (thread 0)
-  uint16_t* cur = q0;
-  uint16_t* nxt = q1;
-  for (uint32_t d = 0;; ++d) {
-    const uint32_t qn = ctrl[C_QN];
+  uint16_t* cur = q0;  // this level: cur[0, qn); the next is appended behind it
+  // One barrier per level: level d reads its size from ctrl[C_LVL + d % 3], counts
+  // the next level into ctrl[C_LVL + (d + 1) % 3], and clears ctrl[C_LVL + (d + 2) % 3]
+  // (read at level d - 1, before the last barrier; next counted at level d + 1, after
+  // the coming one).
+  for (uint32_t d = 0, l3 = 0;; ++d, l3 = l3 == 2 ? 0 : l3 + 1) {
+    const uint32_t qn = ctrl[C_LVL + l3];
     if (qn == 0) break;
     if (d + 1 >= 255) { errf |= ERR_DEPTH; break; }
+    const uint32_t l3n = l3 == 2 ? 0 : l3 + 1, l3c = l3n == 2 ? 0 : l3n + 1;
+    if (tid == 0) ctrl[C_LVL + l3c] = 0;
+    uint16_t* nxt = cur + qn;
     unsigned long long tl0 = (a.phase_clk && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
     for (uint32_t i0 = 0; i0 < qn; i0 += RWG_THREADS) {
       if (i0 + (wid << 6) >= qn) continue;  // wave-uniform: no frontier node for this wave
@@ -611,7 +670,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
           hops_l[row[s]] = (uint8_t)(d + 1);
         }
       const uint32_t k = __popc(newm);
-      uint32_t idx = k ? atomicAdd(&ctrl[C_NEXT], k) : 0;
+      uint32_t idx = k ? atomicAdd(&ctrl[C_LVL + l3n], k) : 0;
 #pragma unroll
       for (int s = 0; s < ASZP; ++s)
         if ((newm >> s) & 1u) nxt[idx++] = (uint16_t)row[s];
@@ -627,12 +686,10 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
       tl0 = t1;
     }
     __syncthreads();
-    if (tid == 0) { ctrl[C_QN] = ctrl[C_NEXT]; ctrl[C_NEXT] = 0; }
-    uint16_t* t = cur; cur = nxt; nxt = t;
-    __syncthreads();
+    cur += qn;
     if (a.phase_clk && tid == 0) {
       prof[4] += 1;  // levels
-      prof[3] += __builtin_amdgcn_s_memtime() - tl0;  // the two barriers
+      prof[3] += __builtin_amdgcn_s_memtime() - tl0;  // the barrier
     }
   }
 
@@ -656,54 +713,44 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
     if (v < N) off_l[v] = b + incl - c;
   }
   __syncthreads();
+  // Every visited node scatters its id into its peers' segments. Only loads and LDS
+  // work here: the per-pair global stores and accumulator atomics are issued at the
+  // end of the kernel (F), since VMEM operations complete in order and a load issued
+  // behind them waits for them. Two nodes per thread per step, both rows in flight.
+  uint8_t* eg_l = smem + L.eg;
   {
-    uint32_t vis = 0, pushes = 0, sc = 0;
-    uint64_t ss = 0;
-    for (uint32_t v = tid; v < N; v += RWG_THREADS) {
-      const size_t p = base + v;
-      const uint32_t h = hops_l[v], c = cnt_l[v];
-      const uint32_t pmv = h != 0xFF ? pm_l[v] : 0u;
-      const uint32_t eg = __popc(pmv);
-      // the row load goes out before this node's stores and atomics: VMEM counts
-      // complete in order, so a load issued after them would wait for them too
-      uint32_t row[ASZP];
-      if (pmv) load_row<ASZP>(a.peers + (size_t)(v * NB + (nl_l[v] >> 11)) * ASZP, row);
-      nts(&a.hops[p], (uint8_t)h);
-      nts(&a.cnt[p], c);
-      nts(&a.egress[p], (uint8_t)eg);
-      if (a.record) {  // measured-round statistics (gossip_main.rs:480-514)
-        pushes += c;
-        if (c) atomicAdd(&a.ingress_acc[p], c);  // fire-and-forget: no load round trip
-        if (eg) atomicAdd(&a.egress_acc[p], eg);
-        if (h != 0xFF) {
-          ++vis;
-          atomicAdd(&hist[h], 1u);
-        } else if (!(nf && a.frank[v] < nf)) {
-          atomicAdd(&a.strand[p], 1u);
-          ++sc;
-          ss += a.stake[v];
-          const uint32_t r = a.srank[v];
-          atomicOr(&bm_l[r >> 5], 1u << (r & 31));
-        }
-      }
-      if (pmv) {
+    uint32_t* dummy = scr + lane;
+    for (uint32_t v0 = tid; v0 < N; v0 += 2 * RWG_THREADS) {
+      const uint32_t v1 = v0 + RWG_THREADS;
+      const uint32_t pm0 = hops_l[v0] != 0xFF ? pm_l[v0] : 0u;
+      const uint32_t pm1 = v1 < N && hops_l[v1] != 0xFF ? pm_l[v1] : 0u;
+      uint32_t r0[ASZP], r1[ASZP];
+      if (pm0) load_row<ASZP>(a.peers + (size_t)(v0 * NB + (nl_l[v0] >> 11)) * ASZP, r0);
+      if (pm1) load_row<ASZP>(a.peers + (size_t)(v1 * NB + (nl_l[v1] >> 11)) * ASZP, r1);
+      eg_l[v0] = (uint8_t)__popc(pm0);
+      if (v1 < N) eg_l[v1] = (uint8_t)__popc(pm1);
+      if (pm0) {
         uint32_t pos[ASZP];
-        uint32_t* dummy = scr + lane;
 #pragma unroll
         for (int s = 0; s < ASZP; ++s) {
-          const bool pu = (pmv >> s) & 1u;
-          pos[s] = atomicAdd(pu ? &off_l[row[s]] : dummy, pu ? 1u : 0u);
+          const bool pu = (pm0 >> s) & 1u;
+          pos[s] = off_fetch_inc<OFF16>(offw, r0[s], pu, dummy);
         }
 #pragma unroll
         for (int s = 0; s < ASZP; ++s)
-          if ((pmv >> s) & 1u) rec_l[pos[s]] = (uint16_t)v;
+          if ((pm0 >> s) & 1u) rec_l[pos[s]] = (uint16_t)v0;
       }
-    }
-    if (a.record) {
-      if (vis) atomicAdd(&ctrl[C_VIS], vis);
-      if (pushes) atomicAdd(&ctrl[C_PUSH], pushes);
-      if (sc) atomicAdd(&ctrl[C_STR], sc);
-      if (ss) atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[C_SSUM]), (unsigned long long)ss);
+      if (pm1) {
+        uint32_t pos[ASZP];
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s) {
+          const bool pu = (pm1 >> s) & 1u;
+          pos[s] = off_fetch_inc<OFF16>(offw, r1[s], pu, dummy);
+        }
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s)
+          if ((pm1 >> s) & 1u) rec_l[pos[s]] = (uint16_t)v1;
+      }
     }
   }
   __syncthreads();
@@ -727,13 +774,13 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
     uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
     if (c) consume_lane(a, p, rec_l + (off_l[v] - c), hops_l, c, len, up, errf);
     if (up >= MIN_NUM_UPSERTS) {
-      if (len > LANE_L) {
+      if (len > (uint32_t)LANE_L) {
         nts(&a.cmeta[p], len | (up << 8));
         hv_l[N - 1 - atomicAdd(&ctrl[C_NHP], 1u)] = (uint16_t)v;
         continue;
       }
       const uint64_t sv = a.stake[v];
-      const uint32_t npr = prune_lane<ASZP>(a, base, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr));
+      const uint32_t npr = prune_lane<ASZP>(a, mkw, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr));
       npr_sum += npr;
       finish_node(a, p, meta, len, 0, npr, true);
     } else {
@@ -762,7 +809,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
       uint32_t npr = 0;
       if (due) {
         const uint64_t sv = a.stake[v];
-        npr = prune_wave<ASZP>(a, base, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr), scr);
+        npr = prune_wave<ASZP>(a, mkw, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr), scr);
         if (lane == 0) npr_sum += npr;
       }
       if (lane == 0) finish_node(a, p, meta, len, due ? 0u : up, npr, due);
@@ -770,6 +817,48 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   }
   if (npr_sum) atomicAdd(&ctrl[C_PRUNES], npr_sum);
   if (errf) atomicOr(&ctrl[C_ERR], errf);
+
+  // ---------------- F: per-pair outputs and measured-round statistics --------
+  // (gossip_main.rs:480-514) Stranded nodes' stake/rank loads go first, then only
+  // stores and fire-and-forget atomics.
+  if (a.record) {
+    uint32_t sc = 0;
+    uint64_t ss = 0;
+    for (uint32_t v = tid; v < N; v += RWG_THREADS) {
+      if (hops_l[v] != 0xFF || (nf && a.frank[v] < nf)) continue;
+      ++sc;
+      ss += a.stake[v];
+      const uint32_t r = a.srank[v];
+      atomicOr(&bm_l[r >> 5], 1u << (r & 31));
+    }
+    if (sc) atomicAdd(&ctrl[C_STR], sc);
+    if (ss) atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[C_SSUM]), (unsigned long long)ss);
+  }
+  {
+    uint32_t vis = 0, pushes = 0;
+    for (uint32_t v = tid; v < N; v += RWG_THREADS) {
+      const size_t p = base + v;
+      const uint32_t h = hops_l[v], c = cnt_l[v], eg = eg_l[v];
+      nts(&a.hops[p], (uint8_t)h);
+      nts(&a.cnt[p], c);
+      nts(&a.egress[p], (uint8_t)eg);
+      if (a.record) {
+        pushes += c;
+        if (c) atomicAdd(&a.ingress_acc[p], c);
+        if (eg) atomicAdd(&a.egress_acc[p], eg);
+        if (h != 0xFF) {
+          ++vis;
+          atomicAdd(&hist[h], 1u);
+        } else if (!(nf && a.frank[v] < nf)) {
+          atomicAdd(&a.strand[p], 1u);
+        }
+      }
+    }
+    if (a.record) {
+      if (vis) atomicAdd(&ctrl[C_VIS], vis);
+      if (pushes) atomicAdd(&ctrl[C_PUSH], pushes);
+    }
+  }
   __syncthreads();
   RWG_MARK(4);
 
@@ -778,6 +867,8 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
     a.slot_prunes[o] = ctrl[C_PRUNES];
     if (ctrl[C_ERR]) atomicOr(a.err, ctrl[C_ERR]);
   }
+  if (ctrl[C_PRUNES] || ctrl[C_MDIRTY])  // prunes / a rotation's clear changed the LDS masks: write back
+    for (uint32_t v = tid; v < N; v += RWG_THREADS) nts(&a.mask[base + v], (uint32_t)mk_l[v]);
   if (!a.record) return;
   for (uint32_t i = tid; i < 256; i += RWG_THREADS)
     if (hist[i]) a.hist_acc[(size_t)o * 256 + i] += hist[i];
@@ -814,7 +905,19 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   RWG_MARK(5);
 }
 
-hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_slot) {
+template <int ASZP, bool OFF16>
+static hipError_t launch_rwg(Engine& e, const RoundArgs& a, size_t lds) {
+  if (e.rwg_attr_lds != lds) {
+    hipError_t r = hipFuncSetAttribute((const void*)k_round_wg<ASZP, OFF16>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (r != hipSuccess) return r;
+    e.rwg_attr_lds = lds;
+  }
+  hipLaunchKernelGGL((k_round_wg<ASZP, OFF16>), dim3(e.S), dim3(RWG_THREADS), lds, e.st, a);
+  return hipSuccess;
+}
+
+hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_slot, bool rot_clear) {
   RoundArgs a;
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.frank = e.frank; a.srank = e.srank;
   a.by_srank = e.by_srank; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake; a.origin = e.origin;
@@ -823,16 +926,17 @@ hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_slot) {
   a.egress = e.egress; a.prune_round = e.prune_round; a.egress_acc = e.egress_acc; a.ingress_acc = e.ingress_acc;
   a.prune_acc = e.prune_acc; a.strand = e.strand; a.hist_acc = e.hist_acc;
   a.sum = record ? e.sum + (size_t)rec_slot * e.S : nullptr;
+  a.rot_list = e.rot_list;
+  a.rot_count = rot_clear ? e.rot_count + e.rot_parity : nullptr;
+  a.rot_changed = e.rot_changed;
   a.err = e.err; a.phase_clk = e.phase_clk;
   a.wave_c_max = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) ? 24u : 64u; a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.fanout = e.fanout; a.fcap = e.fcap; a.PAIRS = e.PAIRS;
   a.record = record ? 1 : 0;
   const size_t lds = round_wg_lds_bytes(e.N, e.fcap, e.ASZP);
   hipError_t r;
-  GS_ASZP_DISPATCH(e.ASZP, {
-    r = hipFuncSetAttribute((const void*)k_round_wg<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (r != hipSuccess) return r;
-    hipLaunchKernelGGL(k_round_wg<A>, dim3(e.S), dim3(RWG_THREADS), lds, e.st, a);
-  });
+  const bool off16 = rwg_off16(e.N, e.fcap);
+  GS_ASZP_DISPATCH(e.ASZP, r = (off16 ? launch_rwg<A, true>(e, a, lds) : launch_rwg<A, false>(e, a, lds)));
+  if (r != hipSuccess) return r;
   return hipGetLastError();
 }
 

@@ -9,7 +9,7 @@ if [ -z "$NO_TEST" ]; then
   tail -5 gpurun_out/ab_pytest.log
   [ $rc -ne 0 ] && exit $rc
 fi
-for v in main ${VARIANTS}; do
+for v in ${ORDER:-main ${VARIANTS}}; do
   if [ "$v" = main ]; then unset GS_LIB_VARIANT; else export GS_LIB_VARIANT=$v; fi
   timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/ab_$v.log 2>&1 || { echo "bench $v rc=$?"; tail -5 gpurun_out/ab_$v.log; exit 1; }
   python3 -c "

@@ -189,6 +189,38 @@ def test_parity_small_fanout_and_asz():
     run_parity(150, [1, 4], 30, p=0.05, mode=gs.GS_BFS_WORKGROUP, asz=7, fanout=3, full_every=5)
 
 
+def test_rotation_round_sequence_and_deferred_clear():
+    """Rotations at repeated / skipped round indices (the rotation counters alternate by
+    round parity), and the one-kernel round's deferred prune-bit clear (applied inside
+    the next round kernel, or flushed before a step call or readback): active sets and
+    prune state stay identical to the oracle's."""
+    n, asz, p = 220, 12, 0.25
+    eng, sims, origins, st = make_pair(n, [1, 9, 50], asz=asz, p=p, mode=gs.GS_BFS_WORKGROUP)
+    assert eng.info()["fused_round"]
+
+    def oracle_round(r, rotate_round):
+        for s, o in zip(sims, origins):
+            s.run_gossip(o)
+            s.consume_messages(o)
+            s.send_prunes(o, 0.15, 2)
+            s.prune_connections()
+            s.chance_to_rotate(asz, p, rotate_round)
+
+    seq = [0, 1, 1, 4, 5, 5, 6, 9, 10, 11, 12, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26]
+    for i, r in enumerate(seq):
+        if i % 3 == 2:  # step-wise iteration: flushes the fused round's pending clear first
+            eng.run_gossip(); eng.consume_messages(); eng.send_prunes(); eng.prune_connections()
+            eng.chance_to_rotate(r)
+        else:
+            eng.round(r)
+        oracle_round(r, r)
+        if i % 4 == 3 or i == len(seq) - 1:
+            assert_entries(eng, sims[0], asz)
+            for k, (s, o) in enumerate(zip(sims, origins)):
+                np.testing.assert_array_equal(eng.pruned_all(k), s.pruned_all(o), err_msg=f"iteration {i}")
+                np.testing.assert_array_equal(eng.distances(k), s.distances())
+
+
 def test_fused_round_matches_steps():
     """gs_round (fused consume+prune+apply) == the step-by-step calls."""
     pks, st = eb.synth.network(260)
