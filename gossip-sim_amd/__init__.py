@@ -71,6 +71,7 @@ class SimConfig(C.Structure):
 EXPORTS = {
     # name: (restype, argtypes)
     "gs_last_error": (C.c_char_p, []),
+    "gs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "gs_create": (C.c_int, [C.POINTER(Params), C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p)]),
     "gs_destroy": (None, [C.c_void_p]),
     "gs_set_slots": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),

@@ -127,6 +127,13 @@ extern "C" {
 
 const char* gs_last_error(void) { return g_err.c_str(); }
 
+int gs_device_count(int* n) {
+  if (!n) return fail(GS_EINVAL, "null argument");
+  *n = 0;
+  if (hipGetDeviceCount(n) != hipSuccess) *n = 0;
+  return GS_OK;
+}
+
 int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t n_slots, gs_engine** out) {
   if (!prm || !stakes || !out) return fail(GS_EINVAL, "null argument");
   *out = nullptr;

@@ -101,6 +101,7 @@ int gs_create(const gs_params* params, const uint64_t* stakes, uint32_t n_nodes,
               gs_engine** out);
 void gs_destroy(gs_engine* e);
 const char* gs_last_error(void);
+int gs_device_count(int* n); /* HIP devices visible to this process (0 without a GPU) */
 int gs_set_slots(gs_engine* e, const gs_slot* slots, uint32_t n_slots);
 int gs_sync(gs_engine* e); /* waits for the stream and reports deferred device-side errors */
 
