@@ -1,0 +1,455 @@
+// gs_consume_g.hip -- consume + prune for the level-synchronous rounds (large N).
+//
+// gs_round's step-kernel path (BFS modes LEVEL / BINNED) leaves each pair's inbound
+// records in HBM as rows inb[j][pair] = hop << 24 | src (j < in-degree). Per pair:
+//   consume_messages + ReceivedCache::record (gossip.rs:618-653, received_cache.rs:27-36,
+//   83-98): the records sorted by (hop, id) -- their u32 order -- in registers by a
+//   sorting network, looked up in the cache entry whose rows are streamed 8 at a time,
+//   coalesced across lanes;
+//   send_prunes + ReceivedCache::prune + prune_connections (gossip.rs:657-737,
+//   received_cache.rs:38-63,100-131) for the entries that reached 20 upserts, from a
+//   worklist: the (score, stake) order as one 31-bit key per entry sorted in registers,
+//   pre-add cumulative stake, prune bits set in the prunees' masks.
+// In-degree > 16 (consume) or entries > 16 keys (prune) are taken by the whole wave,
+// one pair at a time, after the wave's lanes finish their own pairs; in-degree > 64 by
+// an ordered single-lane selection. Results are identical to the generic per-pair code
+// in gs_kernels.hip (cp_generic), which remains the step-wise gs_consume_messages /
+// gs_send_prunes / gs_prune_connections.
+#include <algorithm>
+
+#include "gs_device.h"
+#include "gs_internal.h"
+
+namespace gs {
+
+namespace {
+
+constexpr uint32_t CG_THREADS = 256;
+constexpr uint32_t CG_WAVES = CG_THREADS / 64;
+constexpr uint32_t CG_SCR = 128;  // per-wave LDS scratch (u32)
+constexpr uint32_t LANE_L = 16;  // register prune path capacity
+
+struct CgArgs {
+  const uint64_t* stake;
+  const uint8_t* bucket;
+  const uint32_t* peers;
+  const uint16_t* hl;
+  const uint32_t* origin;
+  const uint8_t* obkt;
+  const uint32_t* min_ingress;
+  const double* thr;
+  const uint32_t* prank;
+  const uint32_t* by_prank;
+  const uint64_t* pstake;
+  const uint32_t* cnt;
+  const uint32_t* inb;
+  uint32_t* cmeta;
+  uint32_t* ckey;
+  uint8_t* prune_round;
+  uint32_t* slot_prunes;
+  uint32_t* mask;
+  uint32_t* ingress_acc;
+  uint32_t* prune_acc;
+  uint32_t* err;
+  uint32_t* work;        // pairs whose prune is due
+  uint32_t* work_count;
+  uint32_t N, S, ASZ, capin;
+  uint32_t lane_c, lane_l, wave_c;  // register-path bounds (16, 16) and wave-consume bound (64);
+                                    // GS_FLAG_NARROW_WAVE_PATH: (4, 4, 8), so small tests reach every path
+  size_t PAIRS;
+  int record;
+};
+
+template <class T>
+__device__ inline T ntl(const T* p) { return __builtin_nontemporal_load(p); }
+
+template <int NC>
+__device__ inline uint32_t match24(const uint32_t (&rk)[16], uint32_t k) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) m |= (uint32_t)((rk[j] & CK_ID) == k) << j;
+  return m;
+}
+
+// Appends p to the due-prune worklist (one atomic per wave).
+__device__ inline void push_work(const CgArgs& a, bool due, uint32_t p) {
+  const unsigned long long bal = __ballot(due);
+  if (!bal) return;
+  const int leader = __ffsll((long long)bal) - 1;
+  uint32_t base = 0;
+  if ((int)lane_id() == leader) base = atomicAdd(a.work_count, (uint32_t)__popcll(bal));
+  base = __shfl(base, leader);
+  if (due) a.work[base + __popcll(bal & ((1ull << lane_id()) - 1))] = p;
+}
+
+// ---- consume, register path (1 <= c <= 16) ----
+__device__ inline void consume_lane(const CgArgs& a, uint32_t q, uint32_t c, uint32_t& len, uint32_t& up,
+                                    uint32_t& errf) {
+  const size_t PAIRS = a.PAIRS;
+  uint32_t rk[16];
+  const uint32_t wc = active_max<5>(c);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) rk[j] = (uint32_t)j < wc ? ntl(&(a.inb + (size_t)j * PAIRS)[q]) : 0xFFFFFFFFu;
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int j = 0; j < 16; ++j) rk[j] = (uint32_t)j < c ? rk[j] : 0xFFFFFFFFu;
+  if (wc <= 4) sort_net<4>(rk);
+  else if (wc <= 8) sort_net<8>(rk);
+  else sort_net<16>(rk);
+  uint32_t present = 0, w0 = 0, w1 = 0;
+  int idx0 = -1, idx1 = -1;
+  const uint32_t wl = active_max<7>(len);
+  for (uint32_t i0 = 0; i0 < wl; i0 += 8) {
+    uint32_t kc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) kc[t] = i0 + t < wl ? ntl(&(a.ckey + (size_t)(i0 + t) * PAIRS)[q]) : 0u;
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const uint32_t i = i0 + t;
+      const uint32_t k = i < len ? ck_id(kc[t]) : 0xFFFFFFFFu;
+      const uint32_t m = wc <= 4 ? match24<4>(rk, k) : wc <= 8 ? match24<8>(rk, k) : match24<16>(rk, k);
+      present |= m;
+      if (m & 1u) { idx0 = (int)i; w0 = kc[t]; }
+      if (m & 2u) { idx1 = (int)i; w1 = kc[t]; }
+    }
+  }
+  up = up < 255 ? up + 1 : 255;  // rank 0 (received_cache.rs:84-86)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {  // timely: score += 1, inserted regardless of the 50-key cap
+    if ((uint32_t)j >= c) break;
+    const int idx = j == 0 ? idx0 : idx1;
+    if (idx >= 0) {
+      (a.ckey + (size_t)idx * PAIRS)[q] = ck_bump(j == 0 ? w0 : w1);
+    } else if (len < CACHE_CAP) {
+      (a.ckey + (size_t)len * PAIRS)[q] = ck_make(rk[j] & CK_ID, 1u);
+      ++len;
+    } else {
+      errf |= ERR_CACHE;
+    }
+  }
+#pragma unroll
+  for (int j = 2; j < 16; ++j)  // rank order; inserted only while len < 50 (received_cache.rs:91-97)
+    if ((uint32_t)j < c && !((present >> j) & 1u) && len < CACHE_LIMIT) {
+      (a.ckey + (size_t)len * PAIRS)[q] = ck_make(rk[j] & CK_ID, 0u);
+      ++len;
+    }
+}
+
+// ---- consume, wave path (16 < c <= 64): all lanes on pair q; len/up wave-uniform ----
+__device__ inline void consume_wave(const CgArgs& a, uint32_t q, uint32_t c, uint32_t& len, uint32_t& up,
+                                    uint32_t* scr, uint32_t& errf) {
+  const size_t PAIRS = a.PAIRS;
+  const uint32_t l = lane_id();
+  uint32_t key = l < c ? (a.inb + (size_t)l * PAIRS)[q] : 0xFFFFFFFFu;
+#pragma unroll
+  for (uint32_t k = 2; k <= 64; k <<= 1)  // bitonic sort across the wave, ascending by lane
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t other = (uint32_t)__shfl_xor((int)key, (int)j);
+      const bool asc = (l & k) == 0;
+      const bool lower = (l & j) == 0;
+      key = (lower == asc) ? min(key, other) : max(key, other);
+    }
+  const uint32_t src = key & CK_ID;
+  const uint32_t L0 = len;
+  for (uint32_t i = l; i < L0; i += 64) scr[i] = (a.ckey + (size_t)i * PAIRS)[q];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  int found = -1;
+  if (l < c)
+    for (uint32_t i = 0; i < L0; ++i)
+      if (ck_id(scr[i]) == src) found = (int)i;
+  const bool isnew = l < c && found < 0;
+  const uint64_t nb = __ballot(isnew);
+  const uint32_t n0 = (uint32_t)(nb & 1u), n1 = (uint32_t)((nb >> 1) & 1u);
+  up = up < 255 ? up + 1 : 255;
+  if (l < 2) {
+    if (found >= 0) {
+      (a.ckey + (size_t)found * PAIRS)[q] = ck_bump(scr[found]);
+    } else {
+      const uint32_t pos = L0 + (l == 1 ? n0 : 0u);
+      if (pos < CACHE_CAP) (a.ckey + (size_t)pos * PAIRS)[q] = ck_make(src, 1u);
+      else errf |= ERR_CACHE;
+    }
+  }
+  const uint32_t L1 = min(L0 + n0 + n1, CACHE_CAP);
+  const uint64_t rest = nb & ~3ull;
+  if (l >= 2 && isnew) {
+    const uint32_t pos = L1 + (uint32_t)__popcll(rest & ((1ull << l) - 1));
+    if (pos < CACHE_LIMIT) (a.ckey + (size_t)pos * PAIRS)[q] = ck_make(src, 0u);
+  }
+  const uint32_t nrest = (uint32_t)__popcll(rest);
+  len = L1 + (L1 < CACHE_LIMIT ? min(nrest, CACHE_LIMIT - L1) : 0u);
+}
+
+// ---- consume, any in-degree (c > 64): lane 0, records selected in order ----
+__device__ inline void consume_serial(const CgArgs& a, uint32_t q, uint32_t c, uint32_t& len, uint32_t& up,
+                                      uint32_t& errf) {
+  const size_t PAIRS = a.PAIRS;
+  uint32_t ln = len, u = up;
+  if (lane_id() == 0) {
+    uint32_t prev = 0;
+    u = u < 255 ? u + 1 : 255;
+    for (uint32_t k = 0; k < c; ++k) {
+      uint32_t best = 0xFFFFFFFFu;
+      for (uint32_t j = 0; j < c; ++j) {
+        const uint32_t r = a.inb[(size_t)j * PAIRS + q];
+        if ((k == 0 || r > prev) && r < best) best = r;
+      }
+      prev = best;
+      const uint32_t src = best & CK_ID;
+      int found = -1;
+      for (uint32_t i = 0; i < ln; ++i)
+        if (ck_id(a.ckey[(size_t)i * PAIRS + q]) == src) { found = (int)i; break; }
+      if (k < 2) {
+        if (found >= 0) {
+          uint32_t* sp = a.ckey + (size_t)found * PAIRS + q;
+          *sp = ck_bump(*sp);
+        } else if (ln < CACHE_CAP) {
+          a.ckey[(size_t)ln * PAIRS + q] = ck_make(src, 1u);
+          ++ln;
+        } else {
+          errf |= ERR_CACHE;
+        }
+      } else if (found < 0 && ln < CACHE_LIMIT) {
+        a.ckey[(size_t)ln * PAIRS + q] = ck_make(src, 0u);
+        ++ln;
+      }
+    }
+  }
+  len = (uint32_t)__shfl((int)ln, 0);
+  up = (uint32_t)__shfl((int)u, 0);
+}
+
+// After a pair's consume: record its in-degree, queue a due prune, else clear the
+// previous round's pruned-len and prune count.
+__device__ inline void after_consume(const CgArgs& a, uint32_t q, uint32_t meta, uint32_t c, uint32_t len,
+                                     uint32_t up, bool& due) {
+  due = up >= MIN_NUM_UPSERTS;
+  const uint32_t nm = due ? (len | (up << 8) | (meta & 0xFF0000u)) : (len | (up << 8));
+  if (nm != meta) a.cmeta[q] = nm;
+  if (!due) a.prune_round[q] = 0;
+  if (a.record && c) a.ingress_acc[q] += c;
+}
+
+// PushActiveSet::prune (push_active_set.rs:56-71,143-151) for (prunee u, pruner v) of slot o.
+template <int ASZP>
+__device__ inline void apply_prune(const CgArgs& a, uint32_t o, uint32_t ob, uint32_t u, uint32_t v) {
+  const uint32_t ent = u * NB + min((uint32_t)a.bucket[u], ob);
+  const uint32_t hv = a.hl[ent];
+  const uint32_t head = hv & 0xFF, L = hv >> 8;
+  uint32_t row[ASZP];
+  load_row<ASZP>(a.peers + (size_t)ent * ASZP, row);
+  uint32_t hit = 0;
+#pragma unroll
+  for (int s = 0; s < ASZP; ++s) {
+    const uint32_t pos = (uint32_t)s >= head ? (uint32_t)s - head : (uint32_t)s + a.ASZ - head;
+    hit |= (uint32_t)((uint32_t)s < a.ASZ && pos < L && row[s] == v) << s;
+  }
+  if (hit) atomicOr(&a.mask[(size_t)o * a.N + u], hit);
+}
+
+// ---- prune, register path (len <= 16) ----
+template <int ASZP>
+__device__ inline uint32_t prune_lane(const CgArgs& a, uint32_t q, uint32_t o, uint32_t v, uint32_t len) {
+  const size_t PAIRS = a.PAIRS;
+  const uint32_t org = a.origin[o], ob = a.obkt[o], mi = a.min_ingress[o];
+  const uint64_t sv = a.stake[v], so = a.stake[org];
+  const uint64_t mis = min_ingress_stake(sv < so ? sv : so, a.thr[o]);
+  const uint32_t wl = active_max<5>(len);
+  uint32_t sk[LANE_L];
+  {
+#pragma unroll
+    for (int i = 0; i < (int)LANE_L; ++i) sk[i] = (uint32_t)i < wl ? ntl(&(a.ckey + (size_t)i * PAIRS)[q]) : 0u;
+    asm volatile("" ::: "memory");
+    uint32_t pr[LANE_L];
+#pragma unroll
+    for (int i = 0; i < (int)LANE_L; ++i) pr[i] = (uint32_t)i < wl ? a.prank[(uint32_t)i < len ? ck_id(sk[i]) : 0u] : 0u;
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < (int)LANE_L; ++i)
+      sk[i] = (uint32_t)i < len ? (((0x7Fu - ck_score(sk[i])) << 24) | pr[i]) : 0xFFFFFFFFu;
+  }
+  if (wl <= 8) sort_net<8>(sk);
+  else sort_net<LANE_L>(sk);
+  // sorted_unstable_by_key(Reverse((score, stake))), ties by id; pre-add cumulative stake;
+  // skip(min_ingress_nodes); skip_while(cum < min_ingress_stake)
+  uint64_t cum = 0;
+  uint32_t npr = 0;
+  bool tail = false;
+#pragma unroll
+  for (int c0 = 0; c0 < (int)LANE_L; c0 += 8) {
+    if ((uint32_t)c0 >= wl) break;
+    uint32_t nd[8];
+    uint64_t st[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const uint32_t i = c0 + t, r = i < len ? sk[c0 + t] & 0xFFFFFFu : 0u;
+      nd[t] = a.by_prank[r];
+      st[t] = a.pstake[r];
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const uint32_t i = c0 + t;
+      if (i < len) {
+        tail = tail || (i >= mi && cum >= mis);
+        const bool pruned = tail && nd[t] != org;
+        npr += pruned;
+        (a.ckey + (size_t)i * PAIRS)[q] = ck_make(nd[t], (0x7Fu - (sk[c0 + t] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
+        if (pruned) apply_prune<ASZP>(a, o, ob, nd[t], v);
+        cum = sat_add(cum, st[t]);
+      }
+    }
+  }
+  return npr;
+}
+
+// ---- prune, wave path (16 < len <= 96): two entries per lane ----
+template <int ASZP>
+__device__ inline uint32_t prune_wave(const CgArgs& a, uint32_t q, uint32_t o, uint32_t v, uint32_t len,
+                                      uint32_t* scr) {
+  const size_t PAIRS = a.PAIRS;
+  const uint32_t l = lane_id();
+  const uint32_t org = a.origin[o], ob = a.obkt[o], mi = a.min_ingress[o];
+  const uint64_t sv = a.stake[v], so = a.stake[org];
+  const uint64_t mis = min_ingress_stake(sv < so ? sv : so, a.thr[o]);
+  uint32_t sk[2], nd[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t i = l + 64 * t;
+    sk[t] = 0xFFFFFFFFu;
+    nd[t] = 0;
+    if (i < len) {
+      const uint32_t w = (a.ckey + (size_t)i * PAIRS)[q];
+      nd[t] = ck_id(w);
+      sk[t] = ((0x7Fu - ck_score(w)) << 24) | a.prank[nd[t]];
+    }
+    scr[i] = sk[t];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  uint32_t rank[2] = {0, 0};
+  uint64_t cum[2] = {0, 0};
+  for (uint32_t j = 0; j < len; ++j) {
+    const uint32_t x = scr[j];
+    const uint64_t st = a.pstake[x & 0xFFFFFFu];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      if (x < sk[t]) { ++rank[t]; cum[t] = sat_add(cum[t], st); }  // saturating sums are order-free
+  }
+  uint32_t npr = 0;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t i = l + 64 * t;
+    bool pruned = false;
+    if (i < len) {
+      pruned = rank[t] >= mi && cum[t] >= mis && nd[t] != org;
+      (a.ckey + (size_t)rank[t] * PAIRS)[q] = ck_make(nd[t], (0x7Fu - (sk[t] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
+      if (pruned) apply_prune<ASZP>(a, o, ob, nd[t], v);
+    }
+    npr += (uint32_t)__popcll(__ballot(pruned));
+  }
+  return npr;
+}
+
+__device__ inline void finish_prune(const CgArgs& a, uint32_t q, uint32_t o, uint32_t len, uint32_t npr) {
+  a.cmeta[q] = len << 16;  // std::mem::take: entry reset, the pruned keys stay readable
+  a.prune_round[q] = (uint8_t)(npr < 255 ? npr : 255);
+  if (npr) {
+    atomicAdd(&a.slot_prunes[o], npr);
+    if (a.record) a.prune_acc[q] += npr;
+  }
+}
+
+// Kernel 1: consume every pair, queue due prunes. Pairs with in-degree > 16 are taken
+// by the whole wave after its lanes finish their own pairs.
+__global__ __launch_bounds__(CG_THREADS) void k_cg_consume(CgArgs a) {
+  __shared__ uint32_t scr_all[CG_WAVES * CG_SCR];
+  uint32_t* scr = scr_all + (threadIdx.x >> 6) * CG_SCR;
+  uint32_t errf = 0;
+  const uint32_t P = (uint32_t)a.PAIRS;
+  for (uint32_t p0 = blockIdx.x * CG_THREADS; p0 < P; p0 += gridDim.x * CG_THREADS) {
+    const uint32_t q = p0 + threadIdx.x;
+    const bool in = q < P;
+    const uint32_t meta = in ? ntl(&a.cmeta[q]) : 0u;
+    uint32_t c = in ? a.cnt[q] : 0u;
+    if (c > a.capin) c = a.capin;
+    uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
+    const bool heavy = in && c > a.lane_c;
+    bool due = false;
+    if (in && !heavy) {
+      if (c) consume_lane(a, q, c, len, up, errf);
+      after_consume(a, q, meta, c, len, up, due);
+    }
+    push_work(a, due, q);
+    uint64_t hv = __ballot(heavy);
+    while (hv) {  // the wave's heavy pairs, one at a time
+      const int l = __ffsll((long long)hv) - 1;
+      hv &= hv - 1;
+      const uint32_t hq = (uint32_t)__shfl((int)q, l);
+      const uint32_t hmeta = (uint32_t)__shfl((int)meta, l);
+      const uint32_t hc = (uint32_t)__shfl((int)c, l);
+      uint32_t hlen = hmeta & 0xFF, hup = (hmeta >> 8) & 0xFF;
+      if (hc <= a.wave_c) consume_wave(a, hq, hc, hlen, hup, scr, errf);
+      else consume_serial(a, hq, hc, hlen, hup, errf);
+      bool hdue = false;
+      if (lane_id() == 0) after_consume(a, hq, hmeta, hc, hlen, hup, hdue);
+      push_work(a, hdue, hq);
+    }
+  }
+  if (errf) atomicOr(a.err, errf);
+}
+
+// Kernel 2: send_prunes + prune_connections of the queued pairs.
+template <int ASZP>
+__global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
+  __shared__ uint32_t scr_all[CG_WAVES * CG_SCR];
+  uint32_t* scr = scr_all + (threadIdx.x >> 6) * CG_SCR;
+  const uint32_t n = *a.work_count;
+  for (uint32_t i0 = blockIdx.x * CG_THREADS; i0 < n; i0 += gridDim.x * CG_THREADS) {
+    const uint32_t i = i0 + threadIdx.x;
+    const bool in = i < n;
+    const uint32_t q = in ? a.work[i] : 0u;
+    const uint32_t o = q / a.N, v = q - o * a.N;
+    const uint32_t len = in ? (a.cmeta[q] & 0xFF) : 0u;
+    const bool heavy = in && len > a.lane_l;
+    if (in && !heavy) finish_prune(a, q, o, len, prune_lane<ASZP>(a, q, o, v, len));
+    uint64_t hv = __ballot(heavy);
+    while (hv) {
+      const int l = __ffsll((long long)hv) - 1;
+      hv &= hv - 1;
+      const uint32_t hq = (uint32_t)__shfl((int)q, l);
+      const uint32_t ho = hq / a.N, hvn = hq - ho * a.N;
+      const uint32_t hlen = (uint32_t)__shfl((int)len, l);
+      const uint32_t npr = prune_wave<ASZP>(a, hq, ho, hvn, hlen, scr);
+      if (lane_id() == 0) finish_prune(a, hq, ho, hlen, npr);
+    }
+  }
+}
+
+}  // namespace
+
+// consume_messages + send_prunes + prune_connections of every slot (gs_round's step path).
+hipError_t launch_consume_prune_g(Engine& e, bool record) {
+  CgArgs a;
+  a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
+  a.min_ingress = e.min_ingress; a.thr = e.thr; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake;
+  a.cnt = e.cnt; a.inb = e.inb; a.cmeta = e.cmeta; a.ckey = e.ckey; a.prune_round = e.prune_round;
+  a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc;
+  a.err = e.err; a.work = e.work; a.work_count = e.work_count;
+  a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.capin = e.capin; a.PAIRS = e.PAIRS; a.record = record ? 1 : 0;
+  const bool narrow = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) != 0;
+  a.lane_c = narrow ? 4u : 16u;
+  a.lane_l = narrow ? 4u : LANE_L;
+  a.wave_c = narrow ? 8u : 64u;
+  hipError_t r;  // (slot_prunes was zeroed by launch_consume_prune)
+  if ((r = hipMemsetAsync(e.work_count, 0, 4, e.st)) != hipSuccess) return r;
+  const uint32_t grid = (uint32_t)std::min<size_t>((e.PAIRS + CG_THREADS - 1) / CG_THREADS, 8192);
+  hipLaunchKernelGGL(k_cg_consume, dim3(grid), dim3(CG_THREADS), 0, e.st, a);
+  GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_cg_prune<A>, dim3(grid), dim3(CG_THREADS), 0, e.st, a));
+  return hipGetLastError();
+}
+
+}  // namespace gs

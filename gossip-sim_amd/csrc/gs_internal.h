@@ -133,6 +133,7 @@ hipError_t launch_bfs(Engine& e, bool record);
 hipError_t launch_bfs_binned(Engine& e, bool record);
 hipError_t launch_bfs_level_step(Engine& e, bool record, uint32_t d, uint32_t qmin, uint32_t qmax);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
+hipError_t launch_consume_prune_g(Engine& e, bool record);
 // Rotation of round `round` (decide + entries); the prune-bit clear of the replaced
 // ring slots runs now, or with defer_clear it is left pending for the next one-kernel
 // round (which applies it to its LDS copy of the masks) or launch_rotate_clear.

@@ -66,8 +66,10 @@ typedef struct gs_params {
                                    gs_round launches the step kernels instead of the one-kernel
                                    workgroup round (same results; for A/B measurement);
                                    GS_FLAG_NARROW_WAVE_PATH: the one-kernel round sends in-degrees
-                                   > 24 (not > 64) to its ordered single-lane consume (same results;
-                                   lets small test clusters cover that path);
+                                   > 24 (not > 64) to its ordered single-lane consume, and the
+                                   step-kernel round uses register paths for in-degree / entries
+                                   <= 4 (not 16) and the wave consume for in-degree <= 8 (not 64)
+                                   (same results; lets small test clusters cover every path);
                                    GS_FLAG_BINNED_ALL_LEVELS: GS_BFS_BINNED bins every level, not
                                    only levels with >= 2^17 frontier pairs (same results) */
 } gs_params;

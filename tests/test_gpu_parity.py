@@ -221,13 +221,17 @@ def test_rotation_round_sequence_and_deferred_clear():
                 np.testing.assert_array_equal(eng.distances(k), s.distances())
 
 
-def test_fused_round_matches_steps():
-    """gs_round (fused consume+prune+apply) == the step-by-step calls."""
+@pytest.mark.parametrize("mode,narrow", [(gs.GS_BFS_LEVEL, False), (gs.GS_BFS_BINNED, False),
+                                         (gs.GS_BFS_LEVEL, True)])
+def test_fused_round_matches_steps(mode, narrow):
+    """gs_round's step-kernel path (consume + prune + apply of gs_consume_g.hip: register,
+    wave and serial consume paths, register and wave prune paths) == the step-by-step
+    calls (the generic per-pair kernels). thresholds 0 / min-ingress 0 make prunes long."""
     pks, st = eb.synth.network(260)
-    a = gs.Engine(st, 4, seed=3, rotation_probability=0.05)
-    b = gs.Engine(st, 4, seed=3, rotation_probability=0.05)
+    a = gs.Engine(st, 4, seed=3, rotation_probability=0.05, narrow_wave_path=narrow, **ekw(mode))
+    b = gs.Engine(st, 4, seed=3, rotation_probability=0.05, **ekw(mode))
     for e in (a, b):
-        e.set_slots([0, 10, 100, 200])
+        e.set_slots([0, 10, 100, 200], [2, 0, 2, 1], [0.15, 0.0, 0.5, 0.05])
         e.init_active_sets()
     for r in range(30):
         a.round(r, record=r >= 10)
