@@ -7,8 +7,8 @@
 //   sorting network, looked up in the cache entry whose rows are streamed 8 at a time,
 //   coalesced across lanes;
 //   send_prunes + ReceivedCache::prune + prune_connections (gossip.rs:657-737,
-//   received_cache.rs:38-63,100-131) for the entries that reached 20 upserts, from a
-//   worklist: the (score, stake) order as one 31-bit key per entry sorted in registers,
+//   received_cache.rs:38-63,100-131) for the entries that reached 20 upserts, found
+//   by a scan of the meta words: the (score, stake) order as one 31-bit key per entry sorted in registers,
 //   pre-add cumulative stake, prune bits set in the prunees' masks.
 // In-degree > 16 (consume) or entries > 16 keys (prune) are taken by the whole wave,
 // one pair at a time, after the wave's lanes finish their own pairs; in-degree > 64 by
@@ -51,8 +51,6 @@ struct CgArgs {
   uint32_t* ingress_acc;
   uint32_t* prune_acc;
   uint32_t* err;
-  uint32_t* work;        // pairs whose prune is due
-  uint32_t* work_count;
   uint32_t N, S, ASZ, capin;
   uint32_t lane_c, lane_l, wave_c;  // register-path bounds (16, 16) and wave-consume bound (64);
                                     // GS_FLAG_NARROW_WAVE_PATH: (4, 4, 8), so small tests reach every path
@@ -69,17 +67,6 @@ __device__ inline uint32_t match24(const uint32_t (&rk)[16], uint32_t k) {
 #pragma unroll
   for (int j = 0; j < NC; ++j) m |= (uint32_t)((rk[j] & CK_ID) == k) << j;
   return m;
-}
-
-// Appends p to the due-prune worklist (one atomic per wave).
-__device__ inline void push_work(const CgArgs& a, bool due, uint32_t p) {
-  const unsigned long long bal = __ballot(due);
-  if (!bal) return;
-  const int leader = __ffsll((long long)bal) - 1;
-  uint32_t base = 0;
-  if ((int)lane_id() == leader) base = atomicAdd(a.work_count, (uint32_t)__popcll(bal));
-  base = __shfl(base, leader);
-  if (due) a.work[base + __popcll(bal & ((1ull << lane_id()) - 1))] = p;
 }
 
 // ---- consume, register path (1 <= c <= 16) ----
@@ -308,8 +295,7 @@ __device__ inline uint32_t prune_lane(const CgArgs& a, uint32_t q, uint32_t o, u
 
 // ---- prune, wave path (16 < len <= 96): two entries per lane ----
 template <int ASZP>
-__device__ inline uint32_t prune_wave(const CgArgs& a, uint32_t q, uint32_t o, uint32_t v, uint32_t len,
-                                      uint32_t* scr) {
+__device__ inline uint32_t prune_wave(const CgArgs& a, uint32_t q, uint32_t o, uint32_t v, uint32_t len) {
   const size_t PAIRS = a.PAIRS;
   const uint32_t l = lane_id();
   const uint32_t org = a.origin[o], ob = a.obkt[o], mi = a.min_ingress[o];
@@ -326,15 +312,21 @@ __device__ inline uint32_t prune_wave(const CgArgs& a, uint32_t q, uint32_t o, u
       nd[t] = ck_id(w);
       sk[t] = ((0x7Fu - ck_score(w)) << 24) | a.prank[nd[t]];
     }
-    scr[i] = sk[t];
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  // every lane's two entries and their stakes go round the wave by shuffles (no
+  // dependent global load per entry)
+  uint64_t stv[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) stv[t] = l + 64 * t < len ? a.pstake[sk[t] & 0xFFFFFFu] : 0ull;
   uint32_t rank[2] = {0, 0};
   uint64_t cum[2] = {0, 0};
   for (uint32_t j = 0; j < len; ++j) {
-    const uint32_t x = scr[j];
-    const uint64_t st = a.pstake[x & 0xFFFFFFu];
+    const bool hi = j >= 64;
+    const int src = (int)(j & 63u);
+    const uint32_t x = (uint32_t)__shfl((int)(hi ? sk[1] : sk[0]), src);
+    const uint64_t sj = hi ? stv[1] : stv[0];
+    const uint32_t slo = (uint32_t)__shfl((int)(uint32_t)sj, src), shi = (uint32_t)__shfl((int)(uint32_t)(sj >> 32), src);
+    const uint64_t st = ((uint64_t)shi << 32) | slo;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
       if (x < sk[t]) { ++rank[t]; cum[t] = sat_add(cum[t], st); }  // saturating sums are order-free
@@ -354,12 +346,24 @@ __device__ inline uint32_t prune_wave(const CgArgs& a, uint32_t q, uint32_t o, u
   return npr;
 }
 
-__device__ inline void finish_prune(const CgArgs& a, uint32_t q, uint32_t o, uint32_t len, uint32_t npr) {
+__device__ inline void finish_prune(const CgArgs& a, uint32_t q, uint32_t len, uint32_t npr) {
   a.cmeta[q] = len << 16;  // std::mem::take: entry reset, the pruned keys stay readable
   a.prune_round[q] = (uint8_t)(npr < 255 ? npr : 255);
-  if (npr) {
+  if (npr && a.record) a.prune_acc[q] += npr;
+}
+
+// Adds each lane's prunee count to its slot's total: one atomic per wave when the
+// wave's pairs share a slot (consecutive pairs do), else one per lane. A per-pair
+// atomic on S counters serializes a prune round (all pairs of a slot hit one word).
+__device__ inline void add_slot_prunes(const CgArgs& a, uint32_t o, uint32_t npr) {
+  const uint32_t o0 = __builtin_amdgcn_readfirstlane(o);
+  if (__ballot(o != o0) == 0) {
+    uint32_t s = npr;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
+    if (lane_id() == 0 && s) atomicAdd(&a.slot_prunes[o0], s);
+  } else if (npr) {
     atomicAdd(&a.slot_prunes[o], npr);
-    if (a.record) a.prune_acc[q] += npr;
   }
 }
 
@@ -383,7 +387,6 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_consume(CgArgs a) {
       if (c) consume_lane(a, q, c, len, up, errf);
       after_consume(a, q, meta, c, len, up, due);
     }
-    push_work(a, due, q);
     uint64_t hv = __ballot(heavy);
     while (hv) {  // the wave's heavy pairs, one at a time
       const int l = __ffsll((long long)hv) - 1;
@@ -396,36 +399,41 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_consume(CgArgs a) {
       else consume_serial(a, hq, hc, hlen, hup, errf);
       bool hdue = false;
       if (lane_id() == 0) after_consume(a, hq, hmeta, hc, hlen, hup, hdue);
-      push_work(a, hdue, hq);
     }
   }
   if (errf) atomicOr(a.err, errf);
 }
 
-// Kernel 2: send_prunes + prune_connections of the queued pairs.
+// Kernel 2: send_prunes + prune_connections of the pairs whose entry reached 20
+// upserts (a scan of the meta words: no contended worklist counter).
 template <int ASZP>
 __global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
-  __shared__ uint32_t scr_all[CG_WAVES * CG_SCR];
-  uint32_t* scr = scr_all + (threadIdx.x >> 6) * CG_SCR;
-  const uint32_t n = *a.work_count;
-  for (uint32_t i0 = blockIdx.x * CG_THREADS; i0 < n; i0 += gridDim.x * CG_THREADS) {
-    const uint32_t i = i0 + threadIdx.x;
-    const bool in = i < n;
-    const uint32_t q = in ? a.work[i] : 0u;
+  const uint32_t P = (uint32_t)a.PAIRS;
+  for (uint32_t p0 = blockIdx.x * CG_THREADS; p0 < P; p0 += gridDim.x * CG_THREADS) {
+    const uint32_t q = p0 + threadIdx.x;
+    const uint32_t meta = q < P ? ntl(&a.cmeta[q]) : 0u;
+    const bool due = q < P && ((meta >> 8) & 0xFF) >= MIN_NUM_UPSERTS;
+    if (!__ballot(due)) continue;
     const uint32_t o = q / a.N, v = q - o * a.N;
-    const uint32_t len = in ? (a.cmeta[q] & 0xFF) : 0u;
-    const bool heavy = in && len > a.lane_l;
-    if (in && !heavy) finish_prune(a, q, o, len, prune_lane<ASZP>(a, q, o, v, len));
+    const uint32_t len = meta & 0xFF;
+    const bool heavy = due && len > a.lane_l;
+    uint32_t npr = 0;
+    if (due && !heavy) {
+      npr = prune_lane<ASZP>(a, q, o, v, len);
+      finish_prune(a, q, len, npr);
+    }
     uint64_t hv = __ballot(heavy);
-    while (hv) {
+    while (hv) {  // the wave's long entries, one at a time
       const int l = __ffsll((long long)hv) - 1;
       hv &= hv - 1;
       const uint32_t hq = (uint32_t)__shfl((int)q, l);
       const uint32_t ho = hq / a.N, hvn = hq - ho * a.N;
       const uint32_t hlen = (uint32_t)__shfl((int)len, l);
-      const uint32_t npr = prune_wave<ASZP>(a, hq, ho, hvn, hlen, scr);
-      if (lane_id() == 0) finish_prune(a, hq, ho, hlen, npr);
+      const uint32_t hn = prune_wave<ASZP>(a, hq, ho, hvn, hlen);
+      if (lane_id() == 0) finish_prune(a, hq, hlen, hn);
+      if ((int)lane_id() == l) npr = hn;
     }
+    add_slot_prunes(a, o, npr);
   }
 }
 
@@ -438,14 +446,13 @@ hipError_t launch_consume_prune_g(Engine& e, bool record) {
   a.min_ingress = e.min_ingress; a.thr = e.thr; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake;
   a.cnt = e.cnt; a.inb = e.inb; a.cmeta = e.cmeta; a.ckey = e.ckey; a.prune_round = e.prune_round;
   a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc;
-  a.err = e.err; a.work = e.work; a.work_count = e.work_count;
+  a.err = e.err;
   a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.capin = e.capin; a.PAIRS = e.PAIRS; a.record = record ? 1 : 0;
   const bool narrow = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) != 0;
   a.lane_c = narrow ? 4u : 16u;
   a.lane_l = narrow ? 4u : LANE_L;
   a.wave_c = narrow ? 8u : 64u;
-  hipError_t r;  // (slot_prunes was zeroed by launch_consume_prune)
-  if ((r = hipMemsetAsync(e.work_count, 0, 4, e.st)) != hipSuccess) return r;
+  // (slot_prunes was zeroed by launch_consume_prune)
   const uint32_t grid = (uint32_t)std::min<size_t>((e.PAIRS + CG_THREADS - 1) / CG_THREADS, 8192);
   hipLaunchKernelGGL(k_cg_consume, dim3(grid), dim3(CG_THREADS), 0, e.st, a);
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_cg_prune<A>, dim3(grid), dim3(CG_THREADS), 0, e.st, a));

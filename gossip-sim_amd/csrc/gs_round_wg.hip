@@ -429,15 +429,21 @@ __device__ inline uint32_t prune_wave(const RoundArgs& a, uint32_t* mkw, const u
       nd[t] = ck_id(w);
       sk[t] = ((0x7Fu - ck_score(w)) << 24) | a.prank[nd[t]];
     }
-    scr[i] = sk[t];
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  // every lane's two entries and their stakes go round the wave by shuffles (no
+  // dependent global load per entry)
+  uint64_t stv[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) stv[t] = l + 64 * t < len ? a.pstake[sk[t] & 0xFFFFFFu] : 0ull;
   uint32_t rank[2] = {0, 0};
   uint64_t cum[2] = {0, 0};
   for (uint32_t j = 0; j < len; ++j) {
-    const uint32_t x = scr[j];
-    const uint64_t st = a.pstake[x & 0xFFFFFFu];
+    const bool hi = j >= 64;
+    const int src = (int)(j & 63u);
+    const uint32_t x = (uint32_t)__shfl((int)(hi ? sk[1] : sk[0]), src);
+    const uint64_t sj = hi ? stv[1] : stv[0];
+    const uint32_t slo = (uint32_t)__shfl((int)(uint32_t)sj, src), shi = (uint32_t)__shfl((int)(uint32_t)(sj >> 32), src);
+    const uint64_t st = ((uint64_t)shi << 32) | slo;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
       if (x < sk[t]) { ++rank[t]; cum[t] = sat_add(cum[t], st); }  // saturating sums are order-free
