@@ -72,6 +72,18 @@ EXPORTS = {
     # name: (restype, argtypes)
     "gs_last_error": (C.c_char_p, []),
     "gs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "gs_part_attach": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "gs_part_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t),
+                                C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "gs_part_begin": (C.c_int, [C.c_void_p]),
+    "gs_part_level": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "gs_part_frontier_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "gs_part_frontier_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "gs_part_consume": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "gs_part_delta_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "gs_part_delta_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "gs_part_stats_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "gs_part_stats_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_create": (C.c_int, [C.POINTER(Params), C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p)]),
     "gs_destroy": (None, [C.c_void_p]),
     "gs_set_slots": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),

@@ -47,7 +47,7 @@ struct CgArgs {
   uint32_t* ckey;
   uint8_t* prune_round;
   uint32_t* slot_prunes;
-  uint32_t* mask;
+  uint32_t* mask;  // prune bits land here: the masks, or a node-range partition's delta
   uint32_t* ingress_acc;
   uint32_t* prune_acc;
   uint32_t* err;
@@ -445,7 +445,7 @@ hipError_t launch_consume_prune_g(Engine& e, bool record) {
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
   a.min_ingress = e.min_ingress; a.thr = e.thr; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake;
   a.cnt = e.cnt; a.inb = e.inb; a.cmeta = e.cmeta; a.ckey = e.ckey; a.prune_round = e.prune_round;
-  a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc;
+  a.slot_prunes = e.slot_prunes; a.mask = e.part_on ? e.part_delta : e.mask; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc;
   a.err = e.err;
   a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.capin = e.capin; a.PAIRS = e.PAIRS; a.record = record ? 1 : 0;
   const bool narrow = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) != 0;

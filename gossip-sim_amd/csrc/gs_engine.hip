@@ -862,4 +862,123 @@ int gs_engine_info(gs_engine* eh, uint32_t* n_nodes, uint32_t* n_slots, uint32_t
   return GS_OK;
 }
 
+// ---------------------------------------------------- node-range partition ----
+#define PART(eh)                                                            \
+  ENGINE(eh);                                                               \
+  if (!e->part_on) return fail(GS_ESTATE, "gs_part_attach has not been called");
+
+static hipMemcpyKind kind_to(int dev) { return dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost; }
+static hipMemcpyKind kind_from(int dev) { return dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice; }
+
+int gs_part_attach(gs_engine* eh, uint32_t rank, uint32_t nranks) {
+  ENGINE(eh);
+  if (nranks < 1 || rank >= nranks) return fail(GS_EINVAL, "rank must be < nranks");
+  if (e->bfs_mode != GS_BFS_LEVEL) return fail(GS_EINVAL, "a node-range partition needs bfs_mode GS_BFS_LEVEL");
+  if (e->part_on) return fail(GS_ESTATE, "already attached");
+  e->part_K = nranks;
+  e->part_rank = rank;
+  e->part_C = (e->N + nranks - 1) / nranks;
+  e->part_lo = std::min(e->N, rank * e->part_C);
+  e->part_hi = std::min(e->N, e->part_lo + e->part_C);
+  e->part_Wr = (e->part_C + 31) / 32;
+  ALLOC(e->part_fr_all, (size_t)nranks * e->S * e->part_Wr, 0);
+  ALLOC(e->part_fr_own, (size_t)e->S * e->part_Wr, 0);
+  ALLOC(e->part_delta, e->PAIRS, 0);
+  ALLOC(e->part_cnt, 2, 0);
+  ALLOC(e->part_stats, part_stats_words(*e), 0);
+  e->part_on = true;
+  return GS_OK;
+}
+
+int gs_part_sizes(gs_engine* eh, size_t* fw, size_t* dw, size_t* sw, uint32_t* lo, uint32_t* hi) {
+  PART(eh);
+  if (fw) *fw = (size_t)e->S * e->part_Wr;
+  if (dw) *dw = e->PAIRS;
+  if (sw) *sw = part_stats_words(*e);
+  if (lo) *lo = e->part_lo;
+  if (hi) *hi = e->part_hi;
+  return GS_OK;
+}
+
+int gs_part_begin(gs_engine* eh) {
+  PART(eh);
+  if (int s = need_slots(e)) return s;
+  if (int s = flush_rot_clear(e)) return s;
+  HIPC(launch_part_begin(*e));
+  return GS_OK;
+}
+
+int gs_part_level(gs_engine* eh, uint32_t level, uint32_t* new_local) {
+  PART(eh);
+  if (!new_local) return fail(GS_EINVAL, "null argument");
+  if (level + 1 >= 255) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
+  HIPC(launch_part_level(*e, level));
+  HIPC(hipMemcpyAsync(e->h_err + 1, e->part_cnt + 1, 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  *new_local = e->h_err[1];
+  e->inb_valid = true;
+  return GS_OK;
+}
+
+int gs_part_frontier_out(gs_engine* eh, void* dst, int dev) {
+  PART(eh);
+  HIPC(hipMemcpyAsync(dst, e->part_fr_own, (size_t)e->S * e->part_Wr * 4, kind_to(dev), e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_part_frontier_in(gs_engine* eh, const void* src, int dev) {
+  PART(eh);
+  HIPC(hipMemcpyAsync(e->part_fr_all, src, (size_t)e->part_K * e->S * e->part_Wr * 4, kind_from(dev), e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_part_consume(gs_engine* eh, uint32_t* local_prunes) {
+  PART(eh);
+  if (!local_prunes) return fail(GS_EINVAL, "null argument");
+  HIPC(hipMemsetAsync(e->part_delta, 0, e->PAIRS * 4, e->st));
+  HIPC(launch_consume_prune(*e, true, true, true, false));  // accumulators: gs_part_stats_out
+  std::vector<uint32_t> sp(e->S);
+  HIPC(hipMemcpyAsync(sp.data(), e->slot_prunes, e->S * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  uint64_t t = 0;
+  for (uint32_t x : sp) t += x;
+  *local_prunes = (uint32_t)std::min<uint64_t>(t, 0xFFFFFFFFu);
+  return GS_OK;
+}
+
+int gs_part_delta_out(gs_engine* eh, void* dst, int dev) {
+  PART(eh);
+  HIPC(hipMemcpyAsync(dst, e->part_delta, e->PAIRS * 4, kind_to(dev), e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_part_delta_in(gs_engine* eh, const void* src, int dev) {
+  PART(eh);
+  HIPC(hipMemcpyAsync(e->part_delta, src, e->PAIRS * 4, kind_from(dev), e->st));
+  HIPC(launch_part_delta_apply(*e));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_part_stats_out(gs_engine* eh, void* dst, int dev) {
+  PART(eh);
+  HIPC(launch_stats(*e, e->sum_used, 3));  // this rank's nodes: partials (and its accumulators)
+  HIPC(launch_part_stats_pack(*e));
+  HIPC(hipMemcpyAsync(dst, e->part_stats, part_stats_words(*e) * 8, kind_to(dev), e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_part_stats_in(gs_engine* eh, const void* src, int dev) {
+  PART(eh);
+  HIPC(hipMemcpyAsync(e->part_stats, src, part_stats_words(*e) * 8, kind_from(dev), e->st));
+  HIPC(launch_part_stats_unpack(*e));
+  HIPC(launch_stats(*e, e->sum_used, 2));  // summary of the summed partials
+  if (++e->sum_used == e->sum_cap) return drain_summaries(e);
+  return GS_OK;
+}
+
 }  // extern "C"

@@ -81,6 +81,14 @@ struct Engine {
   bool rot_have_prev = false;
   uint32_t rot_parity = 0;          // parity of the last rotation's round
   size_t rwg_attr_lds = 0;          // dynamic LDS the round kernel was last configured for
+  // node-range partition (gs_partition.hip): this rank owns node ids [part_lo, part_hi)
+  bool part_on = false;
+  uint32_t part_rank = 0, part_K = 1, part_lo = 0, part_hi = 0, part_C = 0, part_Wr = 0;
+  uint32_t* part_fr_all = nullptr;  // global frontier bitsets [K][S][Wr]
+  uint32_t* part_fr_own = nullptr;  // this rank's next-level bits [S][Wr]
+  uint32_t* part_delta = nullptr;   // prune-mask bits set this round [S][N] (summed over ranks = OR)
+  uint32_t* part_cnt = nullptr;     // [2]: frontier queue length, new local nodes
+  uint64_t* part_stats = nullptr;   // packed stats partials [S][5 + 256 + bm_words]
   // fused consume -> prune worklist
   uint32_t* work = nullptr;
   uint32_t* work_count = nullptr;
@@ -134,6 +142,13 @@ hipError_t launch_bfs_binned(Engine& e, bool record);
 hipError_t launch_bfs_level_step(Engine& e, bool record, uint32_t d, uint32_t qmin, uint32_t qmax);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
 hipError_t launch_consume_prune_g(Engine& e, bool record);
+// node-range partition (gs_partition.hip)
+size_t part_stats_words(const Engine& e);
+hipError_t launch_part_begin(Engine& e);
+hipError_t launch_part_level(Engine& e, uint32_t level);
+hipError_t launch_part_stats_pack(Engine& e);
+hipError_t launch_part_stats_unpack(Engine& e);
+hipError_t launch_part_delta_apply(Engine& e);
 // Rotation of round `round` (decide + entries); the prune-bit clear of the replaced
 // ring slots runs now, or with defer_clear it is left pending for the next one-kernel
 // round (which applies it to its LDS copy of the masks) or launch_rotate_clear.

@@ -882,6 +882,7 @@ struct StatsArgs {
   uint32_t* bm;
   gs_round_summary* sum;
   uint32_t N, S, W;
+  uint32_t lo, hi;  // nodes of this pass (a node-range partition passes its own range)
 };
 
 // FULL: the step-wise gs_record_round (reads the per-round counters of every pair);
@@ -900,7 +901,7 @@ __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
   __syncthreads();
   uint32_t vis = 0, pushes = 0, sc = 0;
   uint64_t ss = 0;
-  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < a.N; v += gridDim.x * blockDim.x) {
+  for (uint32_t v = a.lo + blockIdx.x * blockDim.x + threadIdx.x; v < a.hi; v += gridDim.x * blockDim.x) {
     const size_t p = base + v;
     const uint32_t hh = a.hops[p];
     const uint32_t c = a.cnt[p];
@@ -1032,10 +1033,13 @@ hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   a.egress_acc = e.egress_acc; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc; a.strand = e.strand;
   a.rs_u32 = e.rs_u32; a.rs_ssum = e.rs_ssum; a.rs_hist = e.rs_hist; a.hist_acc = e.hist_acc; a.bm = e.bm;
   a.sum = e.sum; a.N = e.N; a.S = e.S; a.W = e.bm_words;
+  a.lo = e.part_on ? e.part_lo : 0u;
+  a.hi = e.part_on ? e.part_hi : e.N;
   uint32_t gx = grid_for(e.N, 256, 64);
-  if (mode == 0) hipLaunchKernelGGL(k_stats_pass<true>, dim3(gx, e.S), dim3(256), 0, e.st, a);
+  if (mode == 0 || mode == 3) hipLaunchKernelGGL(k_stats_pass<true>, dim3(gx, e.S), dim3(256), 0, e.st, a);
   else if (mode == 1) hipLaunchKernelGGL(k_stats_pass<false>, dim3(gx, e.S), dim3(256), 0, e.st, a);
-  hipLaunchKernelGGL(k_stats_finalize, dim3(e.S), dim3(256), 0, e.st, a, rec_slot);
+  if (mode != 3)  // mode 3: the pass only (a partition sums the partials over ranks first)
+    hipLaunchKernelGGL(k_stats_finalize, dim3(e.S), dim3(256), 0, e.st, a, rec_slot);
   return hipGetLastError();
 }
 

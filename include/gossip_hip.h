@@ -166,6 +166,36 @@ int gs_engine_info(gs_engine* e, uint32_t* n_nodes, uint32_t* n_slots, uint32_t*
  * statistics per slot in one workgroup), 0 if it launches the step kernels. */
 int gs_engine_round_kind(gs_engine* e, uint32_t* fused);
 
+/* --- node-range partition ------------------------------
+ * K engines, one per rank/GPU, each created with bfs_mode GS_BFS_LEVEL on the same
+ * stakes, slots and seed, split the node ids into K equal ranges; rank r owns
+ * [r*C, min((r+1)*C, n)), C = ceil(n / K). Active sets, prune masks and failures are
+ * replicated; per-(slot, node) round state, caches and accumulators are kept for owned
+ * nodes only. One iteration of gossip_main.rs:449-564 is:
+ *   gs_part_begin;
+ *   for level d = 0, 1, ...: gs_part_level(d, &new) -> SUM(new) over ranks; stop at 0;
+ *       else gs_part_frontier_out -> all-gather (rank-major) -> gs_part_frontier_in;
+ *   gs_part_consume(&prunes) -> SUM(prunes); if > 0: gs_part_delta_out -> SUM ->
+ *       gs_part_delta_in;
+ *   gs_chance_to_rotate(round);
+ *   if recorded: gs_part_stats_out -> SUM -> gs_part_stats_in.
+ * The exchanges are the caller's: RCCL all-gather / all-reduce on device buffers over
+ * xGMI, or host buffers (dst_device / src_device select which). Buffers hold u32 words
+ * (frontier, delta) and u64 words (stats); sizes from gs_part_sizes. SUM of the
+ * deltas and of the stranded bitmaps equals their OR: every bit has one owner. */
+int gs_part_attach(gs_engine* e, uint32_t rank, uint32_t nranks);
+int gs_part_sizes(gs_engine* e, size_t* frontier_words /* per rank */, size_t* delta_words,
+                  size_t* stats_words, uint32_t* node_lo, uint32_t* node_hi);
+int gs_part_begin(gs_engine* e);
+int gs_part_level(gs_engine* e, uint32_t level, uint32_t* new_local);
+int gs_part_frontier_out(gs_engine* e, void* dst, int dst_device);       /* [S][Wr] u32 */
+int gs_part_frontier_in(gs_engine* e, const void* src, int src_device);  /* [K][S][Wr] u32 */
+int gs_part_consume(gs_engine* e, uint32_t* local_prunes);
+int gs_part_delta_out(gs_engine* e, void* dst, int dst_device);          /* [S][n] u32 */
+int gs_part_delta_in(gs_engine* e, const void* src, int src_device);
+int gs_part_stats_out(gs_engine* e, void* dst, int dst_device);          /* [S][5 + 256 + W] u64 */
+int gs_part_stats_in(gs_engine* e, const void* src, int src_device);
+
 /* --- host-side statistics (gossip_stats.rs), f64 in the reference's order --- */
 typedef struct gs_hops_stat { double mean, median; uint64_t max, min; } gs_hops_stat;
 typedef struct gs_stat4 { double mean, median, max, min; } gs_stat4;
