@@ -72,6 +72,7 @@ EXPORTS = {
     # name: (restype, argtypes)
     "gs_last_error": (C.c_char_p, []),
     "gs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "gs_read_mst": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "gs_part_attach": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "gs_part_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t),
                                 C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
@@ -348,6 +349,24 @@ class Engine:
                 continue
             _check(rc)
             return out[:cnt.value].reshape(-1, self.n_slots)
+
+    def mst(self, slot):
+        """Cluster::mst (gossip.rs:580-591): {discoverer: sorted nodes it first discovered}."""
+        parent = np.zeros(self.n, dtype=np.uint32)
+        _check(lib().gs_read_mst(self.h, slot, _ptr(parent)))
+        out = {}
+        for v in np.nonzero(parent != 0xFFFFFFFF)[0]:
+            out.setdefault(int(parent[v]), []).append(int(v))
+        return out
+
+    def pushes(self, slot):
+        """Cluster::pushes (gossip.rs:566-573): {src: sorted peers it pushed to}."""
+        off, src, _ = self.inbound(slot)
+        out = {}
+        for v in range(self.n):
+            for s in src[off[v]:off[v + 1]].tolist():
+                out.setdefault(int(s), []).append(v)
+        return {k: sorted(v) for k, v in out.items()}
 
     def accumulators(self, slot):
         e = np.zeros(self.n, dtype=np.uint64)

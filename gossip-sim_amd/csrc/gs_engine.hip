@@ -862,6 +862,73 @@ int gs_engine_info(gs_engine* eh, uint32_t* n_nodes, uint32_t* n_slots, uint32_t
   return GS_OK;
 }
 
+// ----------------------------------------------------------------- MST ----
+// Cluster::mst (gossip.rs:580-591): the first discoverer of every reached node in the
+// reference's FIFO queue order. The queue is level by level; within a level, nodes are
+// in the order (queue position of the discoverer, index of the node in the
+// discoverer's push list = PushActiveSet::get_nodes(..).take(fanout), failed peers
+// included). The discoverer of w is its pusher from the previous level with the
+// smallest queue position. Debug readback, from the step path's inbound records.
+int gs_read_mst(gs_engine* eh, uint32_t slot, uint32_t* parent) {
+  ENGINE(eh);
+  SLOT_CHECK(slot);
+  if (!parent) return fail(GS_EINVAL, "null argument");
+  if (!e->inb_valid)
+    return fail(GS_ESTATE, "inbound records are kept on-chip by the one-kernel gs_round; "
+                           "call gs_run_gossip to materialize them");
+  if (e->N > (1u << 18)) return fail(GS_ERANGE, "gs_read_mst is a debug readback for n <= 262,144");
+  const uint32_t N = e->N, org = e->slots[slot].origin;
+  std::vector<uint8_t> hops(N);
+  if (int s = gs_read_hops(eh, slot, hops.data())) return s;
+  std::vector<uint32_t> cnt(N);
+  HIPC(hipMemcpy(cnt.data(), e->cnt + (size_t)slot * N, N * 4ull, hipMemcpyDeviceToHost));
+  size_t total = 0;
+  for (uint32_t x : cnt) total += std::min(x, e->capin);
+  std::vector<uint32_t> off(N + 1), src(total + 1);
+  std::vector<uint8_t> rh(total + 1);
+  if (int s = gs_read_inbound(eh, slot, off.data(), src.data(), rh.data(), total + 1)) return s;
+  std::vector<uint32_t> peers((size_t)N * NB * e->ASZ), fifo(N);
+  std::vector<uint8_t> lens((size_t)N * NB), bkt(N);
+  if (int s = gs_read_active_sets(eh, peers.data(), lens.data())) return s;
+  if (int s = gs_read_pruned_all(eh, slot, fifo.data())) return s;
+  HIPC(hipMemcpy(bkt.data(), e->bucket, N, hipMemcpyDeviceToHost));
+  // index of w in u's take(fanout) list (get_nodes skips pruned peers and the origin)
+  auto take_index = [&](uint32_t u, uint32_t w) -> uint32_t {
+    const size_t ent = (size_t)u * NB + std::min(bkt[u], bkt[org]);
+    uint32_t t = 0;
+    for (uint32_t i = 0; i < lens[ent] && t < e->fanout; ++i) {
+      const uint32_t p = peers[ent * e->ASZ + i];
+      if (((fifo[u] >> i) & 1u) || p == org) continue;
+      if (p == w) return t;
+      ++t;
+    }
+    return 63;  // not reached for a recorded push
+  };
+  std::vector<uint64_t> pos(N, UINT64_MAX);
+  for (uint32_t v = 0; v < N; ++v) parent[v] = UINT32_MAX;
+  uint32_t maxd = 0;
+  for (uint32_t v = 0; v < N; ++v)
+    if (hops[v] != 0xFF) maxd = std::max<uint32_t>(maxd, hops[v]);
+  std::vector<std::vector<uint32_t>> level(maxd + 1);
+  for (uint32_t v = 0; v < N; ++v)
+    if (hops[v] != 0xFF) level[hops[v]].push_back(v);
+  pos[org] = 0;
+  for (uint32_t d = 1; d <= maxd; ++d) {
+    std::vector<std::pair<uint64_t, uint32_t>> keyed;
+    for (uint32_t w : level[d]) {
+      uint32_t best = UINT32_MAX;
+      for (uint32_t i = off[w]; i < off[w + 1]; ++i)
+        if (rh[i] == d && (best == UINT32_MAX || pos[src[i]] < pos[best])) best = src[i];
+      if (best == UINT32_MAX) return fail(GS_ESTATE, "reached node without a pusher from the previous level");
+      parent[w] = best;
+      keyed.push_back({(pos[best] << 6) | take_index(best, w), w});
+    }
+    std::sort(keyed.begin(), keyed.end());
+    for (size_t r = 0; r < keyed.size(); ++r) pos[keyed[r].second] = r;
+  }
+  return GS_OK;
+}
+
 // ---------------------------------------------------- node-range partition ----
 #define PART(eh)                                                            \
   ENGINE(eh);                                                               \

@@ -157,6 +157,10 @@ int gs_read_round_summaries(gs_engine* e, gs_round_summary* out, size_t cap, siz
 int gs_read_accumulators(gs_engine* e, uint32_t slot, uint64_t* egress, uint64_t* ingress, uint64_t* prunes,
                          uint32_t* stranded_times, uint64_t* hop_hist /*[256]*/);
 int gs_read_failed(gs_engine* e, uint32_t slot, uint8_t* failed /*[n]*/);
+/* Cluster::mst (gossip.rs:580-591): parent[v] = the node that first discovered v in the
+ * reference's FIFO queue order, UINT32_MAX for the origin and unreached nodes (debug
+ * readback after gs_run_gossip, n <= 262,144). */
+int gs_read_mst(gs_engine* e, uint32_t slot, uint32_t* parent /*[n]*/);
 /* GS_FLAG_PROFILE: summed device time of a kernel family ("bfs", "consume",
  * "rotate", "stats") since the last reset, and its launch count. */
 int gs_kernel_time(gs_engine* e, const char* family, double* ms, uint64_t* launches);

@@ -63,6 +63,28 @@ def test_mst_kat_on_gpu(mode):
         assert got[src] == hop
     e, i, p = eng.counters(0)
     assert int(i.sum()) == int(e.sum()) == sum(d["expect_num_inbound"])
+    # the MST asserts of test_mst (gossip.rs:1136-1155): first discoverers in FIFO order
+    mst = {inv[u]: sorted(inv[v] for v in vs) for u, vs in eng.mst(0).items()}
+    assert mst == {5: [2, 4], 4: [0, 3], 0: [1]}
+    # the debug dumps (gossip.rs:365-431) print these records
+    import io
+    import gossip_sim_amd.dumps as dumps
+    keys = [f"K{inv[v]}" for v in range(6)]
+    buf = io.StringIO()
+    dumps.print_mst(eng, 0, keys, out=buf)
+    dumps.print_pushes(eng, 0, keys, out=buf)
+    dumps.print_hops(eng, 0, keys, out=buf)
+    dumps.print_node_orders(eng, 0, keys, out=buf)
+    lines = buf.getvalue().splitlines()
+    assert all(" INFO  gossip_sim::gossip] " in ln for ln in lines)
+    msgs = [ln.split("] ", 1)[1] for ln in lines]
+    assert msgs[0] == "MST: "
+    i5 = msgs.index("##### src: K5 #####")
+    assert sorted(msgs[i5 + 1:i5 + 3]) == ["dest: K2", "dest: K4"]
+    assert "PUSHES: " in msgs and "DISTANCES FROM ORIGIN" in msgs and "NODE ORDERS" in msgs
+    assert "dest node, hops: (K5, 0)" in msgs
+    n_push = sum(len(v) for v in eng.pushes(0).values())
+    assert sum(1 for m in msgs if m.startswith("Dest: ")) == n_push == sum(d["expect_num_inbound"])
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -136,6 +158,12 @@ def run_parity(n, ranks, rounds, *, p, mode, thr=0.15, mi=2, asz=12, fanout=6, f
             for v in range(n):
                 want = s.orders(v)
                 assert lists[v] == ([] if want is None else want), f"inbound slot {k} node {v} round {r}"
+            if r % full_every == 0:  # Cluster::mst (FIFO first discoverers) and Cluster::pushes
+                mst, pushes = eng.mst(k), eng.pushes(k)
+                for u in range(n):
+                    want = s.mst(u)
+                    assert mst.get(u) == (sorted(want) if want else None), f"mst slot {k} src {u} round {r}"
+                    assert pushes.get(u, []) == sorted(s.pushes(u) or []), f"pushes slot {k} src {u} round {r}"
         eng.consume_messages()
         eng.send_prunes()
         for k, (s, o) in enumerate(zip(sims, origins)):
