@@ -1,41 +1,46 @@
 // gs_bfs_binned.hip -- Cluster::run_gossip (gossip.rs:494-615) for large clusters:
-// level-synchronous BFS over every slot at once, propagation-blocked.
+// level-synchronous BFS over every slot at once, propagation-blocked, with the
+// inbound records grouped by destination only once per round.
 //
-// The level kernel k_bfs_level updates a pair's in-degree with a global atomic
-// per push. On gfx950 global atomics execute at the memory side; scattered ones
-// (64 lanes, 64 rows) run ~17x below coalesced ones, so at 1M nodes that one
-// atomic per push is the whole cost of the BFS. Here each level is two kernels
-// and no push touches a global atomic:
+// A push is a scatter: (destination pair, source) lands at a random pair. Scattered
+// global atomics and 4-byte stores cost a 64-128 B memory transaction each on
+// gfx950, so here no push is ever written to its destination directly. Pairs are
+// cut into bins of 2^BS consecutive pair indices; per BFS level:
 //
-//   expand (grid G): workgroup w owns a contiguous slice of the frontier. Pass 1
-//     computes every frontier pair's push mask (the first `fanout` unpruned,
-//     non-origin peers of its active-set entry; failed peers burn a slot) and
-//     counts its pushes per destination bin (2^BS consecutive pairs) in LDS;
-//     an exclusive scan turns the counts into the workgroup's per-bin segment
-//     starts, published as T[b][w]. Pass 2 writes each push record
-//     (destination pair, source node) into its bin segment of the workgroup's
-//     area.
-//   apply (one workgroup per bin): walks the bin's segments of every expand
-//     workgroup. The bin's in-degree counters for THIS level live in LDS (u16),
-//     so a record's arrival index is an LDS atomic; the record lands in inbound
-//     slot cnt[q] + index; a pair's first arrival sets its hop and joins the
-//     next frontier (collected in LDS, appended with one reservation). Finally
-//     the bin's touched counters are added to cnt[] -- the bin owns its pairs,
-//     so plain read-modify-writes suffice.
+//   expand (workgroup w owns frontier positions [w*PW, (w+1)*PW)): loads each
+//     frontier pair's active-set row -- from the compact own-entry table when the
+//     origin's bucket allows (push_active_set.rs:38-52: entry min(bucket[u],
+//     bucket[origin])) -- takes the first `fanout` unpruned, non-origin peers
+//     (failed peers burn a slot), counts pushes per bin in LDS (the atomic's return
+//     is the push's rank in its bin), stages the records sorted by bin in LDS and
+//     writes them out as one contiguous run; T[w][b] = the run's bin starts.
+//   apply (one workgroup per bin, bins dealt to XCDs in contiguous ranges so that
+//     the T rows and area lines a bin reads are shared in its XCD's L2): walks the
+//     bin's segment of every expand workgroup, marks first arrivals in an LDS
+//     bitmap seeded from the bin's hops (first arrival = hop d+1, gossip.rs:594-600),
+//     appends the level's records (local pair, hop<<24 | src) to a pool run of its
+//     own, writes the bin's hops back and appends the new frontier in pair order.
+//   gather (after the last level, one workgroup per bin): counts the bin's records
+//     per pair over all levels, builds the inbound lists as a CSR in LDS and writes
+//     the rows inb[k][pair] (k < in-degree) and the in-degrees cnt[pair] coalesced.
 //
-// Results are identical to k_bfs_level: hops, in-degree, the inbound record
-// SETS per pair (consume sorts them by (hop, src)), egress, frontier sizes.
+// Results equal k_bfs_level's: hops, in-degrees, the inbound record SET of each pair
+// (consume sorts them by (hop, src), gossip.rs:639-645), egress, frontier sizes.
 #include "gs_device.h"
 #include "gs_internal.h"
 
 namespace gs {
 
-constexpr uint32_t BIN_THREADS = 256;
+constexpr uint32_t X_PPT = 4;          // frontier pairs per expand thread
+constexpr uint32_t APPLY_THREADS = 256;
+constexpr uint32_t GATHER_THREADS = 512;
+constexpr uint32_t SEG_CHUNK = 1024;   // expand workgroups' segments scanned per apply chunk
 
 struct BinArgs {
   const uint8_t* bucket;
   const uint32_t* peers;
   const uint16_t* hl;
+  const uint32_t* own;   // [N][ORW] own-bucket entry rows; word ASZP = hl | bucket << 16
   const uint32_t* frank;
   const uint32_t* origin;
   const uint8_t* obkt;
@@ -48,31 +53,39 @@ struct BinArgs {
   uint32_t* egress_acc;
   uint32_t* lvl;
   uint32_t* err;
-  uint32_t* pm;     // push mask per frontier position (pass 1 -> pass 2)
-  uint2* area;      // push records (pair, src) per expand workgroup
-  uint32_t* T;      // [nbins + 1][G] segment starts (row nbins = workgroup totals)
-  uint32_t N, ASZ, fanout, capin, G, BS, nbins, qmin;
-  size_t PAIRS;
+  uint2* area;     // expand -> apply: workgroup w's records (pair, src) sorted by bin at w*PW*fc
+  uint32_t* T;     // [Gmax][nbins + 1] bin starts of each expand workgroup's run (+ its total)
+  uint2* pool;     // apply -> gather: (local pair, hop << 24 | src) runs
+  uint2* Lt;       // [256][nbins] (pool start, count) of bin b's run at level d
+  uint32_t* pool_top;
+  uint32_t* visbm;  // [PAIRS / 32] visited pairs (hop != unreached) of this round
+  uint32_t N, ASZ, fanout, fc, capin, Gmax, PW, BS, nbins, ORW, csr_cap, qmin;
+  size_t PAIRS, pool_cap;
   int record;
 };
 
-__device__ inline void slice_of(uint32_t qn, uint32_t G, uint32_t w, uint32_t& lo, uint32_t& hi) {
-  const uint32_t per = (qn + G - 1) / G;
-  lo = min(qn, w * per);
-  hi = min(qn, lo + per);
+// bins dealt to XCDs in contiguous ranges (workgroup i runs on XCD i % 8)
+__device__ inline uint32_t xcd_bin(uint32_t i, uint32_t nbins) {
+  const uint32_t per = (nbins + 7) / 8;
+  return (i & 7u) * per + (i >> 3);
 }
 
-// the pushes of frontier pair p (gossip.rs:511-541): ring slots taken this round
+// The pushes of frontier pair p (gossip.rs:511-541): ring slots taken this round.
 template <int ASZP>
 __device__ inline uint32_t pair_pushes(const BinArgs& a, uint32_t p, uint32_t (&row)[ASZP], uint32_t& o,
                                        uint32_t& u) {
   o = p / a.N;
   u = p - o * a.N;
-  const uint32_t org = a.origin[o], nf = a.nfail[o];
-  const uint32_t b = min((uint32_t)a.bucket[u], (uint32_t)a.obkt[o]);
-  const uint32_t ent = u * NB + b;
-  const uint32_t hv = a.hl[ent];
-  load_row<ASZP>(a.peers + (size_t)ent * ASZP, row);
+  const uint32_t org = a.origin[o], nf = a.nfail[o], ob = a.obkt[o];
+  const uint32_t* orow = a.own + (size_t)u * a.ORW;
+  load_row<ASZP>(orow, row);
+  const uint32_t meta = orow[ASZP];
+  uint32_t hv = meta & 0xFFFFu;
+  if ((meta >> 16) > ob) {  // the origin's bucket is lower: entry min(bucket[u], bucket[origin])
+    const uint32_t ent = u * NB + ob;
+    hv = a.hl[ent];
+    load_row<ASZP>(a.peers + (size_t)ent * ASZP, row);
+  }
   uint32_t pushm = taken_slots<ASZP>(row, hv & 0xFF, hv >> 8, a.ASZ, a.mask[p], org, a.fanout);
   if (nf) {  // failed peers burn their fanout slot (gossip.rs:538-541)
 #pragma unroll
@@ -82,17 +95,10 @@ __device__ inline uint32_t pair_pushes(const BinArgs& a, uint32_t p, uint32_t (&
   return pushm;
 }
 
-constexpr uint32_t APPLY_THREADS = 256;
-// Levels with fewer frontier pairs than this run k_bfs_level (a global atomic per
-// push is cheap at that size; the binned pair of kernels has a fixed cost).
-// (GS_FLAG_BINNED_ALL_LEVELS: 0, every level binned -- lets small tests cover the kernels.)
-constexpr uint32_t BIN_MIN_FRONTIER = 1u << 17;
-
-// Exclusive scan of LDS counts h[0..n) in place (whole workgroup of THREADS); returns the total.
-template <uint32_t THREADS = BIN_THREADS>
+// Exclusive scan of LDS h[0..n) in place by the whole workgroup; wsum holds 16 words.
 __device__ inline uint32_t block_excl_scan(uint32_t* h, uint32_t n, uint32_t* wsum) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint32_t per = (n + THREADS - 1) / THREADS;
+  const uint32_t TH = blockDim.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = TH >> 6;
+  const uint32_t per = (n + TH - 1) / TH;
   const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
   uint32_t s = 0;
   for (uint32_t i = lo; i < hi; ++i) s += h[i];
@@ -100,7 +106,7 @@ __device__ inline uint32_t block_excl_scan(uint32_t* h, uint32_t n, uint32_t* ws
   if (lane == 63) wsum[wid] = incl;
   __syncthreads();
   uint32_t wb = 0, tot = 0;
-  for (uint32_t k = 0; k < THREADS / 64; ++k) {
+  for (uint32_t k = 0; k < nw; ++k) {
     if (k < wid) wb += wsum[k];
     tot += wsum[k];
   }
@@ -114,151 +120,315 @@ __device__ inline uint32_t block_excl_scan(uint32_t* h, uint32_t n, uint32_t* ws
   return tot;
 }
 
+__host__ __device__ inline size_t bin_expand_lds_bytes(uint32_t nbins, uint32_t PW, uint32_t fc) {
+  return 4 * (size_t)((nbins + 16 + 1) & ~1u) + 8 * (size_t)PW * fc;
+}
+
 template <int ASZP>
-__global__ __launch_bounds__(BIN_THREADS) void k_bin_expand(BinArgs a, uint32_t d, const uint32_t* __restrict__ qcur) {
-  extern __shared__ uint32_t hist[];  // [nbins] + 4 wave sums
+__global__ __launch_bounds__(512) void k_bin_expand(BinArgs a, uint32_t d, const uint32_t* __restrict__ qcur) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t qn = a.lvl[d];
-  if (qn < a.qmin || qn == 0) return;
-  uint32_t lo, hi;
-  slice_of(qn, a.G, blockIdx.x, lo, hi);
-  if (lo >= hi) return;  // apply derives the same slices and skips this workgroup
-  const uint32_t tid = threadIdx.x, w = blockIdx.x;
-  const uint32_t nb = a.nbins, BS = a.BS;
-  for (uint32_t i = tid; i < nb; i += BIN_THREADS) hist[i] = 0;
-  __syncthreads();
-  // pass 1: push masks, per-bin counts
-  for (uint32_t i = lo + tid; i < hi; i += BIN_THREADS) {
-    const uint32_t p = qcur[i];
-    uint32_t row[ASZP], o, u;
-    const uint32_t pushm = pair_pushes<ASZP>(a, p, row, o, u);
-    a.pm[i] = pushm;
-    const uint32_t eg = __popc(pushm);
-    a.egress[p] = (uint8_t)eg;
-    if (a.record && eg) a.egress_acc[p] += eg;
-    const uint32_t qb = o * a.N;
+  if (qn < a.qmin) return;  // k_bin_direct's level
+  const uint32_t G = (qn + a.PW - 1) / a.PW;
+  const uint32_t nb = a.nbins, BS = a.BS, tid = threadIdx.x, TH = blockDim.x;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem);                               // [nb] + 16
+  uint2* stage = reinterpret_cast<uint2*>(smem + 4 * (size_t)((nb + 16 + 1) & ~1u));  // [PW * fc]
+  for (uint32_t w = blockIdx.x; w < G; w += gridDim.x) {  // workgroup slices, grid <= 2 per CU
+    const uint32_t lo = w * a.PW, hi = min(qn, lo + a.PW);
+    for (uint32_t i = tid; i < nb; i += TH) hist[i] = 0;
+    __syncthreads();
+    uint32_t row[X_PPT][ASZP], rk[X_PPT][ASZP], pm[X_PPT], qb[X_PPT], uu[X_PPT];
 #pragma unroll
-    for (int s = 0; s < ASZP; ++s)
-      if ((pushm >> s) & 1u) atomicAdd(&hist[(qb + row[s]) >> BS], 1u);
-  }
-  __syncthreads();
-  const uint32_t total = block_excl_scan(hist, nb, hist + nb);
-  for (uint32_t b = tid; b < nb; b += BIN_THREADS) a.T[(size_t)b * a.G + w] = hist[b];
-  if (tid == 0) a.T[(size_t)nb * a.G + w] = total;
-  __syncthreads();  // every segment start is published before pass 2 advances them
-  // pass 2: records into the bin segments of this workgroup's area
-  uint2* area = a.area + (size_t)lo * min(a.fanout, a.ASZ);
-  for (uint32_t i = lo + tid; i < hi; i += BIN_THREADS) {
-    const uint32_t p = qcur[i];
-    const uint32_t pushm = a.pm[i];
-    const uint32_t o = p / a.N, u = p - o * a.N;
-    const uint32_t b = min((uint32_t)a.bucket[u], (uint32_t)a.obkt[o]);
-    uint32_t row[ASZP];
-    load_row<ASZP>(a.peers + (size_t)(u * NB + b) * ASZP, row);
-    const uint32_t qb = o * a.N;
+    for (uint32_t j = 0; j < X_PPT; ++j) {
+      const uint32_t i = lo + j * TH + tid;
+      pm[j] = 0; qb[j] = 0; uu[j] = 0;
+      if (i < hi) {
+        uint32_t p = qcur[i];
+        if (GS_OOB(p, a.PAIRS, a.err, "binned frontier pair")) p = 0;
+        uint32_t o, u;
+        pm[j] = pair_pushes<ASZP>(a, p, row[j], o, u);
+        const uint32_t eg = __popc(pm[j]);
+        a.egress[p] = (uint8_t)eg;
+        if (a.record && eg) a.egress_acc[p] += eg;
+        qb[j] = o * a.N;
+        uu[j] = u;
+      } else {
 #pragma unroll
-    for (int s = 0; s < ASZP; ++s)
-      if ((pushm >> s) & 1u) {
-        const uint32_t q = qb + row[s];
-        const uint32_t pos = atomicAdd(&hist[q >> BS], 1u);
-        area[pos] = make_uint2(q, u);
+        for (int s = 0; s < ASZP; ++s) row[j][s] = 0;
       }
+    }
+    // every LDS atomic after every load: the rank of each push within its bin
+#pragma unroll
+    for (uint32_t j = 0; j < X_PPT; ++j)
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s)
+        rk[j][s] = ((pm[j] >> s) & 1u) ? atomicAdd(&hist[(qb[j] + row[j][s]) >> BS], 1u) : 0u;
+    __syncthreads();
+    const uint32_t total = block_excl_scan(hist, nb, hist + nb);
+    uint32_t* Tw = a.T + (size_t)w * (nb + 1);
+    for (uint32_t b = tid; b < nb; b += TH) Tw[b] = hist[b];
+    if (tid == 0) Tw[nb] = total;
+#pragma unroll
+    for (uint32_t j = 0; j < X_PPT; ++j)
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s)
+        if ((pm[j] >> s) & 1u) {
+          const uint32_t q = qb[j] + row[j][s];
+          stage[hist[q >> BS] + rk[j][s]] = make_uint2(q, uu[j]);
+        }
+    __syncthreads();
+    uint2* area = a.area + (size_t)w * a.PW * a.fc;
+    for (uint32_t i = tid; i < total; i += TH) area[i] = stage[i];
+    __syncthreads();
   }
 }
 
-// LDS of the apply kernel: segment prefix [G + 1], segment starts [G], the bin's
-// counters [BP] (u32 in-degrees when staged, else packed u16 arrival indices),
-// first arrivals u16 [BP], control words.
-__host__ __device__ inline size_t bin_apply_lds_words(uint32_t G, uint32_t BS) {
-  return 2 * (size_t)G + 1 + ((size_t)1 << BS) + ((size_t)1 << BS) / 2 + 24;
+// Levels with fewer than BIN_MIN_FRONTIER frontier pairs: one thread per frontier pair,
+// a global in-degree atomic per push (cheap when there are few) that also gives the
+// record's inbound slot; first visits from the round's visited bitmap, shared with the
+// binned levels. The gather places the binned levels' records after these slots.
+constexpr uint32_t BIN_MIN_FRONTIER = 1u << 17;
+
+template <int ASZP>
+__global__ __launch_bounds__(256) void k_bin_direct(BinArgs a, uint32_t d, const uint32_t* __restrict__ qcur,
+                                                   uint32_t* __restrict__ qnxt) {
+  const uint32_t qn = a.lvl[d];
+  if (qn >= a.qmin) return;
+  const uint32_t rec_hop = (d + 1) << 24;
+  bool overflow = false;
+  for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < qn; i0 += gridDim.x * blockDim.x) {  // uniform trips
+    const uint32_t i = i0 + threadIdx.x;
+    uint32_t row[ASZP], pm = 0, o = 0, u = 0;
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) row[s] = 0;
+    if (i < qn) {
+      uint32_t p = qcur[i];
+      if (GS_OOB(p, a.PAIRS, a.err, "direct frontier pair")) p = 0;
+      pm = pair_pushes<ASZP>(a, p, row, o, u);
+      const uint32_t eg = __popc(pm);
+      a.egress[p] = (uint8_t)eg;
+      if (a.record && eg) a.egress_acc[p] += eg;
+    }
+    const uint32_t qb = o * a.N;
+    uint32_t slot[ASZP], vold[ASZP];
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) {  // all atomics back to back, then their results
+      const uint32_t q = qb + row[s];
+      const bool on = (pm >> s) & 1u;
+      slot[s] = on ? atomicAdd(&a.cnt[q], 1u) : 0u;
+      vold[s] = on ? atomicOr(&a.visbm[q >> 5], 1u << (q & 31)) : ~0u;
+    }
+    uint32_t newm = 0;
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) {
+      if (!((pm >> s) & 1u)) continue;
+      const uint32_t q = qb + row[s];
+      if (slot[s] < a.capin) a.inb[(size_t)slot[s] * a.PAIRS + q] = rec_hop | u;
+      else overflow = true;
+      if (!((vold[s] >> (q & 31)) & 1u)) {  // first visit: hop = dist[src] + 1 (gossip.rs:594-600)
+        newm |= 1u << s;
+        a.hops[q] = (uint8_t)(d + 1);
+      }
+    }
+    const uint32_t k = __popc(newm);
+    const uint32_t incl = wave_incl_scan(k);
+    const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+    uint32_t qbase = 0;
+    if (lane_id() == 63 && tot) qbase = atomicAdd(&a.lvl[d + 1], tot);
+    uint32_t pos = (uint32_t)__shfl((int)qbase, 63) + incl - k;
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s)
+      if ((newm >> s) & 1u) qnxt[pos++] = qb + row[s];
+  }
+  if (overflow) atomicOr(a.err, ERR_INBOUND);
+}
+
+// apply LDS: pre [SEG_CHUNK + 1], sb [SEG_CHUNK], vis / vis0 bitmaps [BP / 32], control
+__host__ __device__ inline size_t bin_apply_lds_bytes(uint32_t BS) {
+  return 4 * (2 * (size_t)SEG_CHUNK + 1 + 2 * (((size_t)1 << BS) / 32) + 32);
 }
 
 __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t d, uint32_t* __restrict__ qnxt) {
-  extern __shared__ uint32_t smem[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t qn = a.lvl[d];
-  if (qn < a.qmin || qn == 0) return;
-  const uint32_t tid = threadIdx.x, G = a.G;
-  const uint32_t b = blockIdx.x, BP = 1u << a.BS;
-  uint32_t* pre = smem;                                          // [G + 1]
-  uint32_t* sb = pre + G + 1;                                    // [G]
-  uint32_t* cw = sb + G;                                         // [BP]
-  uint16_t* fl = reinterpret_cast<uint16_t*>(cw + BP);           // [BP]
-  uint32_t* ctl = cw + BP + BP / 2;                              // [0] first arrivals, [1] base, [2] overflow, [4..19] scan
-  // 1. this bin's segment in every expand workgroup's area
-  for (uint32_t w = tid; w < G; w += APPLY_THREADS) {
-    uint32_t lo, hi, sz = 0, st = 0;
-    slice_of(qn, G, w, lo, hi);
-    if (lo < hi) {
-      st = a.T[(size_t)b * G + w];
-      sz = a.T[(size_t)(b + 1) * G + w] - st;
-    }
-    pre[w] = sz;
-    sb[w] = st;
-  }
-  if (tid < 3) ctl[tid] = 0;
-  __syncthreads();
-  const uint32_t total = block_excl_scan<APPLY_THREADS>(pre, G, ctl + 4);
-  if (tid == 0) pre[G] = total;
+  if (qn == 0 || qn < a.qmin) return;  // (k_bin_direct's level: no Lt entry, the gather skips it)
+  const uint32_t b = xcd_bin(blockIdx.x, a.nbins);
+  if (b >= a.nbins) return;
+  const uint32_t tid = threadIdx.x, nb = a.nbins, BP = 1u << a.BS, NW = BP / 32;
+  const uint32_t G = (qn + a.PW - 1) / a.PW;
+  uint32_t* pre = reinterpret_cast<uint32_t*>(smem);  // [SEG_CHUNK + 1]
+  uint32_t* sb = pre + SEG_CHUNK + 1;                 // [SEG_CHUNK]
+  uint32_t* vis = sb + SEG_CHUNK;                     // [NW]
+  uint32_t* vis0 = vis + NW;                          // [NW]
+  uint32_t* ctl = vis0 + NW;                          // [0] pool base, [1] frontier base, [2] err, [8..23] scan
   const uint32_t q0 = b << a.BS;
-  const uint32_t qend = (uint32_t)min((size_t)q0 + BP, a.PAIRS);
-  // 2. counters: a busy bin stages its in-degrees (one coalesced read and write);
-  //    a quiet one keeps per-level arrival indices and reads cnt[] per record
-  const bool staged = total >= BP / 4;
-  if (staged) {
-    for (uint32_t i = tid; i < BP; i += APPLY_THREADS) cw[i] = q0 + i < qend ? a.cnt[q0 + i] : 0u;
-  } else {
-    for (uint32_t i = tid; i < BP / 2; i += APPLY_THREADS) cw[i] = 0;
+  // 1. the bin's record count this level (T rows of every expand workgroup)
+  uint32_t cntp = 0;
+  for (uint32_t w = tid; w < G; w += APPLY_THREADS) {
+    const uint32_t* Tw = a.T + (size_t)w * (nb + 1);
+    cntp += Tw[b + 1] - Tw[b];  // starts are exclusive and Tw[nb] is the run's total
+  }
+  {
+    const uint32_t s = wave_incl_scan(cntp);
+    if ((tid & 63) == 63) ctl[8 + (tid >> 6)] = s;
+  }
+  if (tid < NW) {  // the bin's visited bits (hop != unreached)
+    const uint32_t m = a.visbm[(q0 >> 5) + tid];
+    vis[tid] = m;
+    vis0[tid] = m;
   }
   __syncthreads();
-  const uint32_t fc = min(a.fanout, a.ASZ);
-  const uint32_t hop = d + 1;
-  bool overflow = false;
-  // 3. one thread per record
-  for (uint32_t r = tid; r < total; r += APPLY_THREADS) {
-    uint32_t lo = 0, hi = G;  // largest w with pre[w] <= r (a non-empty segment)
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (pre[mid] <= r) lo = mid; else hi = mid;
-    }
-    const uint32_t w = lo;
-    uint32_t wlo, whi;
-    slice_of(qn, G, w, wlo, whi);
-    const uint2 rec = a.area[(size_t)wlo * fc + sb[w] + (r - pre[w])];
-    const uint32_t q = rec.x, ql = q - q0;
-    uint32_t slot;
-    if (staged) {
-      slot = atomicAdd(&cw[ql], 1u);
-    } else {
-      const uint32_t sh = (ql & 1u) << 4;
-      const uint32_t k = (atomicAdd(&cw[ql >> 1], 1u << sh) >> sh) & 0xFFFFu;
-      slot = a.cnt[q] + k;
-    }
-    if (slot < a.capin) a.inb[(size_t)slot * a.PAIRS + q] = (hop << 24) | rec.y;
-    else overflow = true;
-    if (slot == 0) {  // first arrival: hop = dist[src] + 1 (gossip.rs:594-600)
-      a.hops[q] = (uint8_t)hop;
-      fl[atomicAdd(&ctl[0], 1u)] = (uint16_t)ql;
-    }
+  uint32_t total = 0;
+  for (uint32_t k = 0; k < APPLY_THREADS / 64; ++k) total += ctl[8 + k];
+  uint2* Ltd = a.Lt + (size_t)d * nb;
+  if (total == 0) {
+    if (tid == 0) Ltd[b] = make_uint2(0, 0);
+    return;
   }
-  if (overflow) ctl[2] = 1;
-  __syncthreads();
-  const uint32_t nf = ctl[0];
-  if (tid == 0 && nf) ctl[1] = atomicAdd(&a.lvl[d + 1], nf);
-  if (tid == 0 && ctl[2]) atomicOr(a.err, ERR_INBOUND);
-  // 4. the bin's in-degrees after this level
-  if (staged) {
-    for (uint32_t i = tid; q0 + i < qend; i += APPLY_THREADS) a.cnt[q0 + i] = cw[i];
-  } else {
-    for (uint32_t ql = 2 * tid; q0 + ql < qend; ql += 2 * APPLY_THREADS) {
-      const uint32_t c2 = cw[ql >> 1];
-      if (!c2) continue;
-      if (c2 & 0xFFFFu) a.cnt[q0 + ql] += c2 & 0xFFFFu;
-      if ((c2 >> 16) && q0 + ql + 1 < qend) a.cnt[q0 + ql + 1] += c2 >> 16;
-    }
+  // 2. the level's pool run for this bin
+  if (tid == 0) {
+    const uint32_t base = atomicAdd(a.pool_top, total);
+    ctl[0] = base;
+    ctl[2] = 0;
+    if ((size_t)base + total > a.pool_cap) { atomicOr(a.err, ERR_INBOUND); ctl[2] = 1; }
+    Ltd[b] = make_uint2(base, ctl[2] ? 0u : total);
   }
   __syncthreads();
-  // 5. first arrivals join the next frontier
-  const uint32_t base = ctl[1];
-  for (uint32_t i = tid; i < nf; i += APPLY_THREADS) qnxt[base + i] = q0 + fl[i];
+  const uint32_t pbase = ctl[0];
+  const bool pool_ok = ctl[2] == 0;
+  // 3. the records, one thread each, in chunks of SEG_CHUNK expand workgroups
+  const uint32_t rec_hop = (d + 1) << 24;
+  uint32_t done = 0;
+  for (uint32_t c0 = 0; c0 < G; c0 += SEG_CHUNK) {
+    const uint32_t gc = min(SEG_CHUNK, G - c0);
+    for (uint32_t i = tid; i < gc; i += APPLY_THREADS) {
+      const uint32_t* Tw = a.T + (size_t)(c0 + i) * (nb + 1);
+      const uint32_t st = Tw[b];
+      pre[i] = Tw[b + 1] - st;
+      sb[i] = st;
+    }
+    __syncthreads();
+    const uint32_t ct = block_excl_scan(pre, gc, ctl + 8);
+    if (tid == 0) pre[gc] = ct;
+    __syncthreads();
+    for (uint32_t r = tid; r < ct; r += APPLY_THREADS) {
+      uint32_t lo = 0, hi = gc;  // largest i with pre[i] <= r
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= r) lo = mid; else hi = mid;
+      }
+      const uint2 rec = a.area[(size_t)(c0 + lo) * a.PW * a.fc + sb[lo] + (r - pre[lo])];
+      uint32_t ql = rec.x - q0;
+      if (GS_OOB(ql, BP, a.err, "binned record pair")) ql = 0;
+      if (pool_ok) a.pool[pbase + done + r] = make_uint2(ql, rec_hop | rec.y);
+      atomicOr(&vis[ql >> 5], 1u << (ql & 31));
+    }
+    done += ct;
+    __syncthreads();
+  }
+  // 4. first arrivals (hop d + 1) and the next frontier in pair order; one bitmap
+  //    word per thread (NW <= APPLY_THREADS)
+  const uint32_t m = tid < NW ? (vis[tid] & ~vis0[tid]) : 0u;
+  const uint32_t c = __popc(m);
+  const uint32_t incl = wave_incl_scan(c);
+  if ((tid & 63) == 63) ctl[8 + (tid >> 6)] = incl;
+  __syncthreads();
+  uint32_t off = 0, tnew = 0;
+  for (uint32_t k = 0; k < APPLY_THREADS / 64; ++k) {
+    if (k < (tid >> 6)) off += ctl[8 + k];
+    tnew += ctl[8 + k];
+  }
+  if (tnew == 0) return;
+  if (tid == 0) ctl[1] = atomicAdd(&a.lvl[d + 1], tnew);
+  if (m) a.visbm[(q0 >> 5) + tid] = vis[tid];
+  __syncthreads();
+  uint32_t pos = ctl[1] + off + incl - c;
+  for (uint32_t mm = m; mm; mm &= mm - 1) {
+    const uint32_t q = q0 + tid * 32 + __ffs(mm) - 1;
+    qnxt[pos++] = q;
+    a.hops[q] = (uint8_t)(d + 1);
+  }
+}
+
+// gather LDS: direct-level in-degrees [BP], binned counts [BP], CSR cursors [BP], CSR [csr_cap]
+__host__ __device__ inline size_t bin_gather_lds_bytes(uint32_t BS, uint32_t csr_cap) {
+  return 4 * (3 * ((size_t)1 << BS) + (size_t)csr_cap + 32);
+}
+
+// After the last level: the binned levels' records of the bin go to inbound slots after
+// the direct levels' (cnt[pair] so far), rows written coalesced from an LDS CSR; cnt[pair]
+// becomes the round's in-degree.
+__global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t b = xcd_bin(blockIdx.x, a.nbins);
+  if (b >= a.nbins) return;
+  const uint32_t tid = threadIdx.x, nb = a.nbins, BP = 1u << a.BS;
+  uint32_t* cd = reinterpret_cast<uint32_t*>(smem);  // [BP] direct-level in-degree
+  uint32_t* cb = cd + BP;                            // [BP] binned-level records
+  uint32_t* of = cb + BP;                            // [BP] CSR cursor
+  uint32_t* csr = of + BP;                           // [csr_cap]
+  uint32_t* ctl = csr + a.csr_cap;                   // scan words
+  const uint32_t q0 = b << a.BS;
+  const uint32_t nq = (uint32_t)min((size_t)BP, a.PAIRS - q0);
+  for (uint32_t i = tid; i < BP; i += GATHER_THREADS) {
+    cd[i] = i < nq ? a.cnt[q0 + i] : 0u;
+    cb[i] = 0;
+  }
+  __syncthreads();
+  for (uint32_t d = 0; d < 255 && a.lvl[d]; ++d) {
+    if (a.lvl[d] < a.qmin) continue;
+    const uint2 L = a.Lt[(size_t)d * nb + b];
+    for (uint32_t r = tid; r < L.y; r += GATHER_THREADS) atomicAdd(&cb[a.pool[L.x + r].x], 1u);
+  }
+  __syncthreads();
+  uint32_t kmax = 0;
+  bool over = false;
+  for (uint32_t i = tid; i < BP; i += GATHER_THREADS) {
+    const uint32_t c = cb[i];
+    of[i] = c;
+    kmax = max(kmax, c);
+    if (i < nq && c) {
+      a.cnt[q0 + i] = cd[i] + c;
+      over |= cd[i] + c > a.capin;
+    }
+  }
+  if (over) atomicOr(a.err, ERR_INBOUND);
+  for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+  if ((tid & 63) == 0) ctl[16 + (tid >> 6)] = kmax;
+  __syncthreads();
+  kmax = 0;
+  for (uint32_t k = 0; k < GATHER_THREADS / 64; ++k) kmax = max(kmax, ctl[16 + k]);
+  if (kmax == 0) return;
+  const uint32_t E = block_excl_scan(of, BP, ctl);  // of[i] = CSR start of pair i
+  if (E <= a.csr_cap) {
+    for (uint32_t d = 0; d < 255 && a.lvl[d]; ++d) {
+      if (a.lvl[d] < a.qmin) continue;
+      const uint2 L = a.Lt[(size_t)d * nb + b];
+      for (uint32_t r = tid; r < L.y; r += GATHER_THREADS) {
+        const uint2 rec = a.pool[L.x + r];
+        csr[atomicAdd(&of[rec.x], 1u)] = rec.y;
+      }
+    }
+    __syncthreads();  // of[i] is now the END of pair i's list
+    for (uint32_t k = 0; k < kmax; ++k)
+      for (uint32_t i = tid; i < nq; i += GATHER_THREADS) {
+        const uint32_t c = cb[i], slot = cd[i] + k;
+        if (k < c && slot < a.capin) a.inb[(size_t)slot * a.PAIRS + q0 + i] = csr[of[i] - c + k];
+      }
+  } else {  // more records than the LDS CSR holds: place each one directly
+    __syncthreads();
+    for (uint32_t i = tid; i < BP; i += GATHER_THREADS) of[i] = cd[i];
+    __syncthreads();
+    for (uint32_t d = 0; d < 255 && a.lvl[d]; ++d) {
+      if (a.lvl[d] < a.qmin) continue;
+      const uint2 L = a.Lt[(size_t)d * nb + b];
+      for (uint32_t r = tid; r < L.y; r += GATHER_THREADS) {
+        const uint2 rec = a.pool[L.x + r];
+        const uint32_t k = atomicAdd(&of[rec.x], 1u);
+        if (k < a.capin) a.inb[(size_t)k * a.PAIRS + q0 + rec.x] = rec.y;
+      }
+    }
+  }
 }
 
 __global__ void k_bin_seed(BinArgs a, const uint32_t* __restrict__ origin, uint32_t S, uint32_t* q0) {
@@ -266,41 +436,111 @@ __global__ void k_bin_seed(BinArgs a, const uint32_t* __restrict__ origin, uint3
   if (o >= S) return;
   const size_t p = (size_t)o * a.N + origin[o];
   a.hops[p] = 0;
+  atomicOr(&a.visbm[p >> 5], 1u << (p & 31));
   q0[o] = (uint32_t)p;
-  if (o == 0) a.lvl[0] = S;
+  if (o == 0) { a.lvl[0] = S; *a.pool_top = 0; }
 }
 
+}  // namespace gs
+
+namespace gs {
+
+// Own-bucket entry rows (the entry a node uses for every origin whose bucket is at
+// least its own, push_active_set.rs:38-52): own[u] = peers[u][bucket[u]] and, in word
+// ASZP, hl | bucket << 16. Refreshed after init, rotation and entry uploads.
+template <int ASZP>
+__global__ void k_own_rows(const uint8_t* __restrict__ bucket, const uint32_t* __restrict__ peers,
+                           const uint16_t* __restrict__ hl, const uint32_t* __restrict__ list,
+                           const uint32_t* __restrict__ count, uint32_t n_all, uint32_t ORW, uint32_t* __restrict__ own) {
+  const uint32_t n = count ? *count : n_all;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t u = list ? list[i] : i;
+    const uint32_t b = bucket[u];
+    const uint32_t ent = u * NB + b;
+    uint32_t row[ASZP];
+    load_row<ASZP>(peers + (size_t)ent * ASZP, row);
+    uint4* dst = reinterpret_cast<uint4*>(own + (size_t)u * ORW);
+#pragma unroll
+    for (int q = 0; q < ASZP / 4; ++q) dst[q] = make_uint4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+    dst[ASZP / 4] = make_uint4((uint32_t)hl[ent] | (b << 16), 0u, 0u, 0u);
+  }
+}
+
+hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count) {
+  if (!e.own) return hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<size_t>((e.N + 255) / 256, 2048);
+  GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_own_rows<A>, dim3(grid), dim3(256), 0, e.st, e.bucket, e.peers,
+                                              e.hl, list, count, e.N, e.ASZP + 4, e.own));
+  return hipGetLastError();
+}
+
+void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g) {
+  uint32_t lg = 0;
+  while ((1ull << lg) < PAIRS) ++lg;
+  g.BS = std::min(13u, std::max(11u, lg > 13 ? lg - 13 : 0u));  // <= 8192 bins up to 2^26 pairs
+  g.nbins = (uint32_t)((PAIRS + (1ull << g.BS) - 1) >> g.BS);
+  uint32_t pw = 1024;
+  while (pw > 256 && (size_t)pw * fcap * 8 > 48 * 1024) pw >>= 1;  // LDS-staged records <= 48 KiB
+  g.PW = pw;
+  g.Gmax = (uint32_t)((PAIRS + pw - 1) / pw);
+  g.T_words = (size_t)g.Gmax * (g.nbins + 1);
+  // two gather workgroups per CU (LDS <= 80 KiB) for bins of 2^11 pairs, one beyond
+  const size_t budget = g.BS <= 11 ? 80 * 1024 : 160 * 1024;
+  g.csr_cap = (uint32_t)((budget - 4 * (3 * ((size_t)1 << g.BS) + 32)) / 4);
+  (void)N;
+}
+
+bool bin_supported(const BinGeom& g, uint32_t fcap) {
+  return g.T_words * 4 <= (1ull << 30) && bin_expand_lds_bytes(g.nbins, g.PW, fcap) <= 160 * 1024;
+}
 
 hipError_t launch_bfs_binned(Engine& e, bool record) {
   BinArgs a;
-  a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.frank = e.frank; a.origin = e.origin; a.obkt = e.obkt;
-  a.nfail = e.nfail; a.mask = e.mask; a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb; a.egress = e.egress;
-  a.egress_acc = e.egress_acc; a.lvl = e.lvl; a.err = e.err; a.pm = e.bin_pm; a.area = e.bin_area;
-  a.T = e.bin_T; a.N = e.N; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.G = e.bin_G;
-  a.BS = e.bin_BS; a.nbins = e.bin_nb; a.PAIRS = e.PAIRS; a.record = record ? 1 : 0;
-  a.qmin = (e.prm.flags & GS_FLAG_BINNED_ALL_LEVELS) ? 0u : BIN_MIN_FRONTIER;
+  a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.own = e.own; a.frank = e.frank; a.origin = e.origin;
+  a.obkt = e.obkt; a.nfail = e.nfail; a.mask = e.mask; a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb;
+  a.egress = e.egress; a.egress_acc = e.egress_acc; a.lvl = e.lvl; a.err = e.err; a.area = e.bin_area;
+  a.T = e.bin_T; a.pool = e.bin_pool; a.Lt = e.bin_Lt; a.pool_top = e.bin_pool_top;
+  a.visbm = e.bin_vis;
+  a.N = e.N; a.ASZ = e.ASZ; a.fanout = e.fanout; a.fc = e.fcap; a.capin = e.capin; a.Gmax = e.bin.Gmax;
+  a.PW = e.bin.PW; a.BS = e.bin.BS; a.nbins = e.bin.nbins; a.ORW = e.ASZP + 4; a.csr_cap = e.bin.csr_cap;
+  a.qmin = (e.prm.flags & GS_FLAG_BINNED_ALL_LEVELS) ? 1u : BIN_MIN_FRONTIER;
+  a.PAIRS = e.PAIRS; a.pool_cap = e.PAIRS * e.fcap; a.record = record ? 1 : 0;
   hipError_t r;
   if ((r = hipMemsetAsync(e.hops, 0xFF, e.PAIRS, e.st)) != hipSuccess) return r;
-  if ((r = hipMemsetAsync(e.cnt, 0, e.PAIRS * 4, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st)) != hipSuccess) return r;
+  if ((r = hipMemsetAsync(e.cnt, 0, e.PAIRS * 4, e.st)) != hipSuccess) return r;
+  if ((r = hipMemsetAsync(e.bin_vis, 0, (e.PAIRS + 31) / 32 * 4, e.st)) != hipSuccess) return r;
   hipLaunchKernelGGL(k_bin_seed, dim3((e.S + 255) / 256), dim3(256), 0, e.st, a, e.origin, e.S, e.q[0]);
-  const size_t lds_x = ((size_t)e.bin_nb + 4) * 4;
-  const size_t lds_a = bin_apply_lds_words(e.bin_G, e.bin_BS) * 4;
-  r = hipFuncSetAttribute((const void*)k_bin_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a);
+  const size_t lds_x = bin_expand_lds_bytes(a.nbins, a.PW, a.fc);
+  const size_t lds_a = bin_apply_lds_bytes(a.BS);
+  const size_t lds_g = bin_gather_lds_bytes(a.BS, a.csr_cap);
+  const uint32_t xth = a.PW / X_PPT;
+  const uint32_t xgrid = std::min<uint32_t>(a.Gmax, 512);  // slices looped: empty levels cost one wave of workgroups
+  const uint32_t bgrid = ((a.nbins + 7) / 8) * 8;
+  const uint32_t dgrid = (uint32_t)std::min<size_t>(BIN_MIN_FRONTIER / 256, (e.PAIRS + 255) / 256);
+  if ((r = hipFuncSetAttribute((const void*)k_bin_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a)))
+    return r;
+  if ((r = hipFuncSetAttribute((const void*)k_bin_gather, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
+    return r;
+  GS_ASZP_DISPATCH(e.ASZP, {
+    r = hipFuncSetAttribute((const void*)k_bin_expand<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
+  });
   if (r != hipSuccess) return r;
   for (uint32_t d = 0; d < 254; ++d) {
-    if (a.qmin && (r = launch_bfs_level_step(e, record, d, 0, a.qmin)) != hipSuccess) return r;
-    GS_ASZP_DISPATCH(e.ASZP, {
-      r = hipFuncSetAttribute((const void*)k_bin_expand<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
-      if (r != hipSuccess) return r;
-      hipLaunchKernelGGL(k_bin_expand<A>, dim3(e.bin_G), dim3(BIN_THREADS), lds_x, e.st, a, d, e.q[d & 1]);
-    });
-    hipLaunchKernelGGL(k_bin_apply, dim3(e.bin_nb), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
+    if (a.qmin > 1)
+      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_bin_direct<A>, dim3(dgrid), dim3(256), 0, e.st, a, d,
+                                                  e.q[d & 1], e.q[(d + 1) & 1]));
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_bin_expand<A>, dim3(xgrid), dim3(xth), lds_x, e.st, a, d,
+                                                e.q[d & 1]));
+    hipLaunchKernelGGL(k_bin_apply, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
     if ((d & 3) == 3) {  // poll the frontier size every 4 levels
       uint32_t* h = e.h_err + 1;
       if ((r = hipMemcpyAsync(h, e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st)) != hipSuccess) return r;
       if ((r = hipStreamSynchronize(e.st)) != hipSuccess) return r;
-      if (*h == 0) return hipGetLastError();
+      if (*h == 0) {
+        hipLaunchKernelGGL(k_bin_gather, dim3(bgrid), dim3(GATHER_THREADS), lds_g, e.st, a);
+        return hipGetLastError();
+      }
     }
   }
   return hipErrorNotSupported;  // frontier still non-empty after 254 levels: hop counts no longer fit u8

@@ -172,11 +172,13 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   uint32_t mode = prm->bfs_mode;
   const size_t lds = bfs_wg_lds_bytes(n);
   const size_t pairs = (size_t)n * n_slots;
+  bin_geometry(n, pairs, e->fcap, e->bin);
+  const bool bin_ok = pairs <= (1ull << 28) && bin_supported(e->bin, e->fcap);
   if (mode == GS_BFS_AUTO)
-    mode = (n <= 8192 && n_slots >= 64) ? GS_BFS_WORKGROUP : (pairs <= (1ull << 28) ? GS_BFS_BINNED : GS_BFS_LEVEL);
-  if (mode == GS_BFS_BINNED && pairs > (1ull << 28)) {
+    mode = (n <= 8192 && n_slots >= 64) ? GS_BFS_WORKGROUP : (bin_ok ? GS_BFS_BINNED : GS_BFS_LEVEL);
+  if (mode == GS_BFS_BINNED && !bin_ok) {
     destroy_engine(e);
-    return fail(GS_EINVAL, "binned BFS supports n_nodes * n_slots <= 2^28");
+    return fail(GS_EINVAL, "binned BFS: n_nodes * n_slots too large for its bin tables (use GS_BFS_LEVEL)");
   }
   if (mode == GS_BFS_WORKGROUP && (n > 65535 || lds > 160 * 1024)) {
     destroy_engine(e);
@@ -226,14 +228,13 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
     ALLOC(e->q[1], PAIRS, 0);
   }
   if (mode == GS_BFS_BINNED) {  // ~4096 bins of 2^BS consecutive pairs (L2-sized apply working set)
-    uint32_t lg = 0;
-    while ((1ull << lg) < PAIRS) ++lg;
-    e->bin_BS = std::min(14u, std::max(10u, lg > 12 ? lg - 12 : 0u));
-    e->bin_nb = (uint32_t)((PAIRS + (1ull << e->bin_BS) - 1) >> e->bin_BS);
-    e->bin_G = (uint32_t)std::min<size_t>(1024, std::max<size_t>(32, PAIRS / 2048));
-    ALLOC(e->bin_pm, PAIRS, 0);
+    ALLOC(e->own, N * (e->ASZP + 4), 0);
     ALLOC(e->bin_area, PAIRS * e->fcap, 0);
-    ALLOC(e->bin_T, ((size_t)e->bin_nb + 1) * e->bin_G, 0);
+    ALLOC(e->bin_T, e->bin.T_words, 0);
+    ALLOC(e->bin_pool, PAIRS * e->fcap, 0);
+    ALLOC(e->bin_Lt, (size_t)256 * e->bin.nbins, 0);
+    ALLOC(e->bin_pool_top, 1, 0);
+    ALLOC(e->bin_vis, (PAIRS + 31) / 32, 0);
   }
   ALLOC(e->lvl, 256, 0);
   ALLOC(e->rot_list, N, 0);
@@ -373,6 +374,7 @@ int gs_set_active_set_entry(gs_engine* eh, uint32_t node, uint32_t bucket, const
   uint16_t hv = (uint16_t)(len << 8);
   HIPC(hipMemcpyAsync(e->peers + ent * e->ASZP, row.data(), e->ASZP * 4, hipMemcpyHostToDevice, e->st));
   HIPC(hipMemcpyAsync(e->hl + ent, &hv, 2, hipMemcpyHostToDevice, e->st));
+  HIPC(launch_own_rows(*e, nullptr, nullptr));
   HIPC(launch_clear_slot_masks(*e, node, bucket, 0xFFFFFFFFu));
   HIPC(hipStreamSynchronize(e->st));
   return GS_OK;

@@ -20,6 +20,13 @@ namespace gs {
 //                cache meta u32 (len | upserts << 8 | pruned-len << 16),
 //                cache keys u32 [96][pairs], scores u8 [96][pairs] (bit 7 = pruned),
 //                egress/prune-sent of the round u8, measured accumulators u32
+// Geometry of the propagation-blocked BFS (gs_bfs_binned.hip): bins of 2^BS pairs,
+// expand workgroups of PW frontier pairs (at most Gmax of them).
+struct BinGeom {
+  uint32_t BS = 0, nbins = 0, PW = 0, Gmax = 0, csr_cap = 0;
+  size_t T_words = 0;
+};
+
 struct Engine {
   gs_params prm{};
   uint32_t N = 0, S = 0;
@@ -69,10 +76,14 @@ struct Engine {
   uint32_t* q[2] = {nullptr, nullptr};
   uint32_t* lvl = nullptr;  // frontier sizes per level [256]
   // propagation-blocked BFS (GS_BFS_BINNED, gs_bfs_binned.hip)
-  uint32_t* bin_pm = nullptr;   // push mask per frontier position
-  uint2* bin_area = nullptr;    // push records (pair, src), PAIRS * fcap
-  uint32_t* bin_T = nullptr;    // [nbins + 1][G] segment starts
-  uint32_t bin_G = 0, bin_BS = 0, bin_nb = 0;
+  BinGeom bin{};
+  uint32_t* own = nullptr;      // [N][ASZP + 4] own-bucket entry rows (word ASZP = hl | bucket << 16)
+  uint2* bin_area = nullptr;    // expand -> apply records (pair, src), per level, PAIRS * fcap
+  uint32_t* bin_T = nullptr;    // [Gmax][nbins + 1] bin starts of each expand workgroup's run
+  uint2* bin_pool = nullptr;    // apply -> gather records (local pair, hop << 24 | src), PAIRS * fcap
+  uint2* bin_Lt = nullptr;      // [256][nbins] (pool start, count) per level and bin
+  uint32_t* bin_pool_top = nullptr;
+  uint32_t* bin_vis = nullptr;  // [PAIRS / 32] visited bitmap of the round
   // rotation
   uint32_t* rot_list = nullptr;
   uint32_t* rot_count = nullptr;    // [2]: rotation r counts into [r & 1] and zeroes [(r + 1) & 1]
@@ -140,6 +151,10 @@ hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket, ui
 hipError_t launch_bfs(Engine& e, bool record);
 hipError_t launch_bfs_binned(Engine& e, bool record);
 hipError_t launch_bfs_level_step(Engine& e, bool record, uint32_t d, uint32_t qmin, uint32_t qmax);
+void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g);
+bool bin_supported(const BinGeom& g, uint32_t fcap);
+// own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
+hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
 hipError_t launch_consume_prune_g(Engine& e, bool record);
 // node-range partition (gs_partition.hip)

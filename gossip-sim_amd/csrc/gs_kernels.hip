@@ -96,7 +96,8 @@ hipError_t launch_init_entries(Engine& e) {
   const uint32_t total = e.N * NB;
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_init_entries<A>, dim3(grid_for(total, 256)), dim3(256), 0, e.st,
                                               e.bucket, e.P, e.peers, e.hl, e.N, e.ASZ, e.prm.seed));
-  return hipGetLastError();
+  hipError_t r = hipGetLastError();
+  return r != hipSuccess ? r : launch_own_rows(e, nullptr, nullptr);
 }
 
 // ------------------------------------------------------------ fail (R15) ----
@@ -238,6 +239,8 @@ hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear) {
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_rotate_entries<A>, dim3(grid_for((size_t)e.N * NB, 256, 2048)),
                                               dim3(256), 0, e.st, e.bucket, e.P, e.peers, e.hl, e.rot_list, cnt,
                                               e.rot_changed, e.N, e.ASZ, e.prm.seed, round));
+  hipError_t ro = launch_own_rows(e, e.rot_list, cnt);
+  if (ro != hipSuccess) return ro;
   e.rot_parity = par;
   e.rot_have_prev = true;
   e.rot_clear_pending = true;
