@@ -115,20 +115,43 @@ __device__ inline uint32_t prefix_search(const uint64_t* __restrict__ P, uint32_
   return lo;
 }
 
+// prefix_search with a coarse table PS[j] = P[min(j * PS_STRIDE, n)] (L2-resident): the
+// coarse search narrows the answer to one stride of P (2 KiB), the fine one finishes it.
+constexpr uint32_t PS_LOG = 8, PS_STRIDE = 1u << PS_LOG;
+__host__ __device__ inline uint32_t ps_count(uint32_t n) { return (n >> PS_LOG) + 2; }
+__device__ inline uint32_t prefix_search2(const uint64_t* __restrict__ P, const uint64_t* __restrict__ PS,
+                                          uint32_t n, uint64_t x) {
+  // smallest j in [1, m) with PS[j] > x (m: none)
+  const uint32_t m = ps_count(n);
+  uint32_t lo = 1, hi = m;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (PS[mid] > x) hi = mid; else lo = mid + 1;
+  }
+  // answer i = smallest index in [flo, fhi] with P[i] > x; returns i - 1
+  uint32_t flo = (lo - 1) << PS_LOG, fhi = min(n, lo << PS_LOG);
+  flo = flo + 1 < fhi ? flo + 1 : fhi;
+  while (flo < fhi) {
+    const uint32_t mid = (flo + fhi) >> 1;
+    if (P[mid] > x) fhi = mid; else flo = mid + 1;
+  }
+  return flo - 1;
+}
+
 // One WeightedShuffle step over the remaining candidates: given v uniform in
 // [0, sum of remaining weights), return the smallest remaining index whose
 // running prefix exceeds v. `rem` (ascending) lists excluded ids with weights;
 // walking them in order shifts v past each excluded weight lying before the
 // answer, so a single search over the full prefix array finds it.
 template <int R>
-__device__ inline uint32_t shuffle_pick(const uint64_t* __restrict__ P, uint32_t n, uint64_t v,
-                                        const uint32_t (&rem)[R], const uint64_t (&remw)[R], int nr) {
+__device__ inline uint32_t shuffle_pick(const uint64_t* __restrict__ P, const uint64_t* __restrict__ PS, uint32_t n,
+                                        uint64_t v, const uint32_t (&rem)[R], const uint64_t (&remw)[R], int nr) {
   uint64_t x = v;
   for (int i = 0; i < nr; ++i) {
     if (P[rem[i]] <= x) x += remw[i];
     else break;
   }
-  return prefix_search(P, n, x);
+  return prefix_search2(P, PS, n, x);
 }
 
 template <int R>

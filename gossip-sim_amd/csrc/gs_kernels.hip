@@ -25,9 +25,10 @@ static inline uint32_t grid_for(size_t n, uint32_t block, uint32_t cap = 1u << 2
 
 // -------------------------------------------------------------- weights ----
 __global__ __launch_bounds__(1024) void k_prefix_weights(const uint8_t* __restrict__ bucket, uint64_t* __restrict__ P,
-                                                        uint32_t N) {
+                                                        uint64_t* __restrict__ PS, uint32_t N) {
   const int k = blockIdx.x;
   uint64_t* Pk = P + (size_t)k * (N + 1);
+  uint64_t* PSk = PS + (size_t)k * ps_count(N);
   const uint32_t T = blockDim.x, t = threadIdx.x;
   const uint32_t chunk = (N + T - 1) / T;
   const uint32_t lo = min(N, t * chunk), hi = min(N, lo + chunk);
@@ -43,15 +44,19 @@ __global__ __launch_bounds__(1024) void k_prefix_weights(const uint8_t* __restri
     __syncthreads();
   }
   uint64_t run = part[t] - s;
-  if (t == 0) Pk[0] = 0;
+  if (t == 0) { Pk[0] = 0; PSk[0] = 0; }
   for (uint32_t i = lo; i < hi; ++i) {
     run += weight(k, bucket[i]);
     Pk[i + 1] = run;
+    if (((i + 1) & (PS_STRIDE - 1)) == 0) PSk[(i + 1) >> PS_LOG] = run;
+  }
+  if (t == T - 1) {  // samples past the end repeat the total: PS[j] = P[min(j * stride, N)]
+    for (uint32_t j = (N >> PS_LOG) + 1; j < ps_count(N); ++j) PSk[j] = run;
   }
 }
 
 hipError_t launch_prefix_weights(Engine& e) {
-  hipLaunchKernelGGL(k_prefix_weights, dim3(NB), dim3(1024), 0, e.st, e.bucket, e.P, e.N);
+  hipLaunchKernelGGL(k_prefix_weights, dim3(NB), dim3(1024), 0, e.st, e.bucket, e.P, e.PS, e.N);
   return hipGetLastError();
 }
 
@@ -61,13 +66,15 @@ hipError_t launch_prefix_weights(Engine& e) {
 // 2..size+1 (or every candidate when N - 1 <= size).
 template <int ASZP>
 __global__ __launch_bounds__(256) void k_init_entries(const uint8_t* __restrict__ bucket,
-                                                     const uint64_t* __restrict__ P, uint32_t* __restrict__ peers,
+                                                     const uint64_t* __restrict__ P, const uint64_t* __restrict__ PS,
+                                                     uint32_t* __restrict__ peers,
                                                      uint16_t* __restrict__ hl, uint32_t N, uint32_t size,
                                                      uint64_t seed) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= N * NB) return;
   const uint32_t u = gid / NB, k = gid % NB;
   const uint64_t* Pk = P + (size_t)k * (N + 1);
+  const uint64_t* PSk = PS + (size_t)k * ps_count(N);
   constexpr int R = ASZP + 2;
   uint32_t rem[R];
   uint64_t remw[R];
@@ -83,7 +90,7 @@ __global__ __launch_bounds__(256) void k_init_entries(const uint8_t* __restrict_
   uint32_t filled = 0;
   for (uint32_t t = 0; t < T; ++t) {
     const uint64_t v = sample_below(left, s);
-    const uint32_t c = shuffle_pick(Pk, N, v, rem, remw, nr);
+    const uint32_t c = shuffle_pick(Pk, PSk, N, v, rem, remw, nr);
     const uint64_t wc = weight(k, bucket[c]);
     left -= wc;
     rem_insert(rem, remw, nr, c, wc);
@@ -95,7 +102,7 @@ __global__ __launch_bounds__(256) void k_init_entries(const uint8_t* __restrict_
 hipError_t launch_init_entries(Engine& e) {
   const uint32_t total = e.N * NB;
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_init_entries<A>, dim3(grid_for(total, 256)), dim3(256), 0, e.st,
-                                              e.bucket, e.P, e.peers, e.hl, e.N, e.ASZ, e.prm.seed));
+                                              e.bucket, e.P, e.PS, e.peers, e.hl, e.N, e.ASZ, e.prm.seed));
   hipError_t r = hipGetLastError();
   return r != hipSuccess ? r : launch_own_rows(e, nullptr, nullptr);
 }
@@ -136,13 +143,30 @@ hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket_k, 
 }
 
 // ---------------------------------------------------------- rotation (R14) ----
-__global__ void k_rotate_decide(uint32_t N, uint64_t seed, uint32_t round, double p, uint32_t* rot_list,
-                                uint32_t* rot_count, uint32_t* rot_count_other) {
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u == 0) *rot_count_other = 0;  // the next rotation's counter (its last reader ran before this kernel)
-  if (u >= N) return;
-  Philox s(seed, P_DECIDE, u, round);
-  if (unit_f64(s.next()) < p) rot_list[atomicAdd(rot_count, 1u)] = u;
+// Each block decides a contiguous node range and appends its rotating nodes with ONE
+// global atomic (rotation is per node and order-free: rot_list order does not matter).
+__global__ __launch_bounds__(1024) void k_rotate_decide(uint32_t N, uint64_t seed, uint32_t round, double p,
+                                                       uint32_t* rot_list, uint32_t* rot_count,
+                                                       uint32_t* rot_count_other) {
+  __shared__ uint32_t lcount, lbase;
+  __shared__ uint32_t lids[2048];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *rot_count_other = 0;  // the next rotation's counter
+  const uint32_t per = (N + gridDim.x - 1) / gridDim.x;
+  const uint32_t lo = min(N, blockIdx.x * per), hi = min(N, lo + per);
+  for (uint32_t c0 = lo; c0 < hi; c0 += 2048) {  // chunks of at most 2048 nodes fit the LDS list
+    if (threadIdx.x == 0) lcount = 0;
+    __syncthreads();
+    for (uint32_t u = c0 + threadIdx.x; u < min(hi, c0 + 2048); u += blockDim.x) {
+      Philox s(seed, P_DECIDE, u, round);
+      if (unit_f64(s.next()) < p) lids[atomicAdd(&lcount, 1u)] = u;
+    }
+    __syncthreads();
+    const uint32_t n = lcount;
+    if (threadIdx.x == 0 && n) lbase = atomicAdd(rot_count, n);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) rot_list[lbase + i] = lids[i];
+    __syncthreads();
+  }
 }
 
 // One thread per (rotating node, entry k). On a full entry the reference's loop
@@ -150,7 +174,8 @@ __global__ void k_rotate_decide(uint32_t N, uint64_t seed, uint32_t round, doubl
 // then drops the oldest: the ring's head slot is overwritten.
 template <int ASZP>
 __global__ __launch_bounds__(256) void k_rotate_entries(const uint8_t* __restrict__ bucket,
-                                                       const uint64_t* __restrict__ P, uint32_t* __restrict__ peers,
+                                                       const uint64_t* __restrict__ P, const uint64_t* __restrict__ PS,
+                                                       uint32_t* __restrict__ peers,
                                                        uint16_t* __restrict__ hl, const uint32_t* __restrict__ rot_list,
                                                        const uint32_t* __restrict__ rot_count,
                                                        uint32_t* __restrict__ rot_changed, uint32_t N, uint32_t size,
@@ -165,6 +190,7 @@ __global__ __launch_bounds__(256) void k_rotate_entries(const uint8_t* __restric
     const uint32_t S = size;
     uint32_t* row = peers + (size_t)ent * ASZP;
     const uint64_t* Pk = P + (size_t)k * (N + 1);
+    const uint64_t* PSk = PS + (size_t)k * ps_count(N);
     constexpr int R = ASZP + 2;
     uint32_t rem[R];
     uint64_t remw[R];
@@ -176,7 +202,7 @@ __global__ __launch_bounds__(256) void k_rotate_entries(const uint8_t* __restric
     uint32_t changed = 0;
     for (uint32_t drawn = 0; drawn + 1 < N; ++drawn) {
       const uint64_t v = sample_below(left, s);
-      const uint32_t c = shuffle_pick(Pk, N, v, rem, remw, nr);
+      const uint32_t c = shuffle_pick(Pk, PSk, N, v, rem, remw, nr);
       const uint64_t wc = weight(k, bucket[c]);
       left -= wc;
       if (nr < R) rem_insert(rem, remw, nr, c, wc);
@@ -234,10 +260,10 @@ hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear) {
     hipError_t r = hipMemsetAsync(cnt, 0, sizeof(uint32_t), e.st);
     if (r != hipSuccess) return r;
   }
-  hipLaunchKernelGGL(k_rotate_decide, dim3(grid_for(e.N, 256)), dim3(256), 0, e.st, e.N, e.prm.seed, round,
+  hipLaunchKernelGGL(k_rotate_decide, dim3(grid_for(e.N, 4096, 256)), dim3(1024), 0, e.st, e.N, e.prm.seed, round,
                      e.prm.rotation_probability, e.rot_list, cnt, e.rot_count + (par ^ 1u));
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_rotate_entries<A>, dim3(grid_for((size_t)e.N * NB, 256, 2048)),
-                                              dim3(256), 0, e.st, e.bucket, e.P, e.peers, e.hl, e.rot_list, cnt,
+                                              dim3(256), 0, e.st, e.bucket, e.P, e.PS, e.peers, e.hl, e.rot_list, cnt,
                                               e.rot_changed, e.N, e.ASZ, e.prm.seed, round));
   hipError_t ro = launch_own_rows(e, e.rot_list, cnt);
   if (ro != hipSuccess) return ro;
@@ -936,46 +962,43 @@ __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
   if (threadIdx.x == 0 && ssum_s) atomicAdd((unsigned long long*)&a.rs_ssum[o], ssum_s);
 }
 
-// k-th set bit (0-based) of a slot's stranded bitmap, found by the whole block.
-__device__ uint32_t block_kth_bit(const uint32_t* __restrict__ bm, uint32_t W, uint32_t k, uint32_t* scratch) {
+// The k[0..3]-th set bits (0-based) of a slot's stranded bitmap, found by the whole
+// block with ONE prefix pass over the bitmap's per-thread popcounts.
+__device__ void block_kth_bits(const uint32_t* __restrict__ bm, uint32_t W, const uint32_t (&k)[4], uint32_t* scratch,
+                               uint32_t* out) {
   const uint32_t T = blockDim.x, t = threadIdx.x;
   const uint32_t chunk = (W + T - 1) / T;
   const uint32_t lo = min(W, t * chunk), hi = min(W, lo + chunk);
   uint32_t c = 0;
   for (uint32_t i = lo; i < hi; ++i) c += __popc(bm[i]);
-  scratch[t] = c;
+  const uint32_t incl = wave_incl_scan(c);
+  if ((t & 63) == 63) scratch[t >> 6] = incl;
   __syncthreads();
-  for (uint32_t off = 1; off < T; off <<= 1) {
-    const uint32_t x = t >= off ? scratch[t - off] : 0;
-    __syncthreads();
-    scratch[t] += x;
-    __syncthreads();
-  }
-  const uint32_t before = scratch[t] - c;
-  __syncthreads();
-  if (k >= before && k < before + c) {
-    uint32_t need = k - before;
+  uint32_t before = incl - c;
+  for (uint32_t w = 0; w < (t >> 6); ++w) before += scratch[w];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!(k[j] >= before && k[j] < before + c)) continue;
+    uint32_t need = k[j] - before;
     for (uint32_t i = lo; i < hi; ++i) {
       uint32_t w = bm[i];
       const uint32_t pc = __popc(w);
       if (need < pc) {
-        for (uint32_t j = 0; j < need; ++j) w &= w - 1;
-        scratch[T] = i * 32 + (__ffs(w) - 1);
+        for (uint32_t q = 0; q < need; ++q) w &= w - 1;
+        out[j] = i * 32 + (__ffs(w) - 1);
         break;
       }
       need -= pc;
     }
   }
   __syncthreads();
-  const uint32_t r = scratch[T];
-  __syncthreads();
-  return r;
 }
 
-__global__ __launch_bounds__(256) void k_stats_finalize(StatsArgs a, uint32_t rec_slot) {
+__global__ __launch_bounds__(1024) void k_stats_finalize(StatsArgs a, uint32_t rec_slot) {
   const uint32_t o = blockIdx.x;
   __shared__ uint32_t hb[256];
-  __shared__ uint32_t scratch[257];
+  __shared__ uint32_t scratch[16];
+  __shared__ uint32_t kth[4];
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     hb[i] = a.rs_hist[o * 256 + i];
     a.hist_acc[o * 256 + i] += hb[i];
@@ -1011,10 +1034,12 @@ __global__ __launch_bounds__(256) void k_stats_finalize(StatsArgs a, uint32_t re
   const uint32_t sc = s.stranded;
   if (sc) {
     const uint32_t klo = sc % 2 ? sc / 2 : sc / 2 - 1, khi = sc / 2;
-    s.stranded_stake_min = a.stake[a.by_srank[block_kth_bit(bmo, a.W, 0, scratch)]];
-    s.stranded_stake_max = a.stake[a.by_srank[block_kth_bit(bmo, a.W, sc - 1, scratch)]];
-    s.stranded_med_lo = a.stake[a.by_srank[block_kth_bit(bmo, a.W, klo, scratch)]];
-    s.stranded_med_hi = a.stake[a.by_srank[block_kth_bit(bmo, a.W, khi, scratch)]];
+    const uint32_t ks[4] = {0u, sc - 1, klo, khi};
+    block_kth_bits(bmo, a.W, ks, scratch, kth);
+    s.stranded_stake_min = a.stake[a.by_srank[kth[0]]];
+    s.stranded_stake_max = a.stake[a.by_srank[kth[1]]];
+    s.stranded_med_lo = a.stake[a.by_srank[kth[2]]];
+    s.stranded_med_hi = a.stake[a.by_srank[kth[3]]];
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < a.W; i += blockDim.x) a.bm[(size_t)o * a.W + i] = 0;
@@ -1038,11 +1063,11 @@ hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   a.sum = e.sum; a.N = e.N; a.S = e.S; a.W = e.bm_words;
   a.lo = e.part_on ? e.part_lo : 0u;
   a.hi = e.part_on ? e.part_hi : e.N;
-  uint32_t gx = grid_for(e.N, 256, 64);
+  uint32_t gx = grid_for(e.N, 256, std::max<uint32_t>(64, 2048 / std::max<uint32_t>(e.S, 1)));
   if (mode == 0 || mode == 3) hipLaunchKernelGGL(k_stats_pass<true>, dim3(gx, e.S), dim3(256), 0, e.st, a);
   else if (mode == 1) hipLaunchKernelGGL(k_stats_pass<false>, dim3(gx, e.S), dim3(256), 0, e.st, a);
   if (mode != 3)  // mode 3: the pass only (a partition sums the partials over ranks first)
-    hipLaunchKernelGGL(k_stats_finalize, dim3(e.S), dim3(256), 0, e.st, a, rec_slot);
+    hipLaunchKernelGGL(k_stats_finalize, dim3(e.S), dim3(1024), 0, e.st, a, rec_slot);
   return hipGetLastError();
 }
 
