@@ -80,6 +80,42 @@ def cpu_baseline(pks, stakes, args, budget_s):
             "origin_rounds_per_s": rounds / el}
 
 
+def large_leg(gs, synth, args, nodes=1_000_000, slots=8, warmup=5, steps=20):
+    """SURVEY 8(d) C4-shaped secondary measurement (1 GPU): a 1M-node network, 8 origin
+    slots (independent sims, origins = node ids 0..7), the step-kernel round with the binned BFS. Reports the propagation path's
+    B_prop fraction of HBM peak (north-star target) and the whole round's rate."""
+    pks, stakes = synth.network(nodes)
+    eng = gs.Engine(stakes, slots, fanout=args.fanout, active_set_size=args.active_set_size,
+                    rotation_probability=args.rotation_probability, seed=args.seed, device=0, profile=True)
+    eng.set_slots(list(range(slots)), args.min_ingress, args.threshold)
+    eng.init_active_sets()
+    for r in range(warmup):
+        eng.round(r, record=False)
+    eng.sync()
+    eng.kernel_time_reset()
+    t0 = time.perf_counter()
+    for r in range(warmup, warmup + steps):
+        eng.round(r, record=True)
+    eng.sync()
+    dt = time.perf_counter() - t0
+    summ = eng.summaries()
+    E = float(summ["pushes"].astype("float64").sum())
+    V = float(summ["visited"].astype("float64").sum())
+    b_ms, _ = eng.kernel_time("bfs")
+    info = eng.info()
+    eng.close()
+    b_prop = V * (4 * args.active_set_size + 5) + 8 * E
+    ach = b_prop / (b_ms * 1e-3) / 1e9 if b_ms > 0 else None
+    return {"workload": f"C4-shaped: {nodes}-node power-law network, {slots} origin slots, step-kernel round",
+            "bfs_mode": info["bfs_mode"], "steps": steps, "warmup": warmup,
+            "ms_per_step": dt / steps * 1e3, "edges_per_s": E / dt,
+            "bfs_us_per_round": b_ms * 1e3 / steps,
+            "bfs_roofline": {"bound": "hbm", "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+                             "bytes_model": "B_prop (SURVEY 8d)",
+                             "kernels": "k_bin_direct/k_bin_expand/k_bin_apply per level + k_bin_gather"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,6 +134,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--split-round", action="store_true", help="step kernels instead of the one-kernel round")
+    ap.add_argument("--no-large", action="store_true", help="skip the 1M-node secondary leg")
     args = ap.parse_args()
 
     gs = load_pkg()          # loads libgossip_hip.so (and its HIP runtime) before torch, if torch is used at all
@@ -209,6 +246,8 @@ def main():
     eng.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pks, stakes, args, args.cpu_budget)
+    if rank == 0 and world == 1 and not args.no_large and args.nodes < 1_000_000:
+        out["large_1m"] = large_leg(gs, synth, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -53,9 +53,9 @@ struct BinArgs {
   uint32_t* egress_acc;
   uint32_t* lvl;
   uint32_t* err;
-  uint2* area;     // expand -> apply: workgroup w's records (pair, src) sorted by bin at w*PW*fc
+  void* area;      // expand -> apply: workgroup w's records sorted by bin at w*PW*fc (RecW / RecN)
   uint32_t* T;     // [Gmax][nbins + 1] bin starts of each expand workgroup's run (+ its total)
-  uint2* pool;     // apply -> gather: (local pair, hop << 24 | src) runs
+  void* pool;      // apply -> gather: per (level, bin) runs (RecW / RecN)
   uint2* Lt;       // [256][nbins] (pool start, count) of bin b's run at level d
   uint32_t* pool_top;
   uint32_t* visbm;  // [PAIRS / 32] visited pairs (hop != unreached) of this round
@@ -69,6 +69,29 @@ __device__ inline uint32_t xcd_bin(uint32_t i, uint32_t nbins) {
   const uint32_t per = (nbins + 7) / 8;
   return (i & 7u) * per + (i >> 3);
 }
+
+// Record formats. Wide (uint2): area (pair, src), pool (local pair, hop << 24 | src).
+// Narrow (u32, bins of 2^11 pairs and N <= 2^21): area and pool (local pair << 21 | src);
+// the bin is known from the segment/run and the hop from the level.
+constexpr uint32_t NARROW_SRC_BITS = 21, NARROW_BS = 11;
+struct RecW {
+  using T = uint2;
+  __device__ static T area(uint32_t q, uint32_t u, uint32_t) { return make_uint2(q, u); }
+  __device__ static uint32_t area_ql(T r, uint32_t q0) { return r.x - q0; }
+  __device__ static uint32_t area_src(T r) { return r.y; }
+  __device__ static T pool(uint32_t ql, uint32_t hopv, uint32_t src) { return make_uint2(ql, hopv | src); }
+  __device__ static uint32_t pool_ql(T r) { return r.x; }
+  __device__ static uint32_t pool_val(T r, uint32_t) { return r.y; }
+};
+struct RecN {
+  using T = uint32_t;
+  __device__ static T area(uint32_t q, uint32_t u, uint32_t BPm) { return ((q & BPm) << NARROW_SRC_BITS) | u; }
+  __device__ static uint32_t area_ql(T r, uint32_t) { return r >> NARROW_SRC_BITS; }
+  __device__ static uint32_t area_src(T r) { return r & ((1u << NARROW_SRC_BITS) - 1); }
+  __device__ static T pool(uint32_t ql, uint32_t, uint32_t src) { return (ql << NARROW_SRC_BITS) | src; }
+  __device__ static uint32_t pool_ql(T r) { return r >> NARROW_SRC_BITS; }
+  __device__ static uint32_t pool_val(T r, uint32_t hopv) { return hopv | (r & ((1u << NARROW_SRC_BITS) - 1)); }
+};
 
 // The pushes of frontier pair p (gossip.rs:511-541): ring slots taken this round.
 template <int ASZP>
@@ -120,19 +143,21 @@ __device__ inline uint32_t block_excl_scan(uint32_t* h, uint32_t n, uint32_t* ws
   return tot;
 }
 
-__host__ __device__ inline size_t bin_expand_lds_bytes(uint32_t nbins, uint32_t PW, uint32_t fc) {
-  return 4 * (size_t)((nbins + 16 + 1) & ~1u) + 8 * (size_t)PW * fc;
+__host__ __device__ inline size_t bin_expand_lds_bytes(uint32_t nbins, uint32_t PW, uint32_t fc, uint32_t rec_bytes) {
+  return 4 * (size_t)((nbins + 16 + 1) & ~1u) + rec_bytes * (size_t)PW * fc;
 }
 
-template <int ASZP>
+template <int ASZP, class R>
 __global__ __launch_bounds__(512) void k_bin_expand(BinArgs a, uint32_t d, const uint32_t* __restrict__ qcur) {
+  using RT = typename R::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t qn = a.lvl[d];
   if (qn < a.qmin) return;  // k_bin_direct's level
   const uint32_t G = (qn + a.PW - 1) / a.PW;
   const uint32_t nb = a.nbins, BS = a.BS, tid = threadIdx.x, TH = blockDim.x;
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);                               // [nb] + 16
-  uint2* stage = reinterpret_cast<uint2*>(smem + 4 * (size_t)((nb + 16 + 1) & ~1u));  // [PW * fc]
+  RT* stage = reinterpret_cast<RT*>(smem + 4 * (size_t)((nb + 16 + 1) & ~1u));  // [PW * fc]
+  const uint32_t BPm = (1u << BS) - 1;
   for (uint32_t w = blockIdx.x; w < G; w += gridDim.x) {  // workgroup slices, grid <= 2 per CU
     const uint32_t lo = w * a.PW, hi = min(qn, lo + a.PW);
     for (uint32_t i = tid; i < nb; i += TH) hist[i] = 0;
@@ -174,10 +199,10 @@ __global__ __launch_bounds__(512) void k_bin_expand(BinArgs a, uint32_t d, const
       for (int s = 0; s < ASZP; ++s)
         if ((pm[j] >> s) & 1u) {
           const uint32_t q = qb[j] + row[j][s];
-          stage[hist[q >> BS] + rk[j][s]] = make_uint2(q, uu[j]);
+          stage[hist[q >> BS] + rk[j][s]] = R::area(q, uu[j], BPm);
         }
     __syncthreads();
-    uint2* area = a.area + (size_t)w * a.PW * a.fc;
+    RT* area = reinterpret_cast<RT*>(a.area) + (size_t)w * a.PW * a.fc;
     for (uint32_t i = tid; i < total; i += TH) area[i] = stage[i];
     __syncthreads();
   }
@@ -248,7 +273,9 @@ __host__ __device__ inline size_t bin_apply_lds_bytes(uint32_t BS) {
   return 4 * (2 * (size_t)SEG_CHUNK + 1 + 2 * (((size_t)1 << BS) / 32) + 32);
 }
 
+template <class R>
 __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t d, uint32_t* __restrict__ qnxt) {
+  using RT = typename R::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t qn = a.lvl[d];
   if (qn == 0 || qn < a.qmin) return;  // (k_bin_direct's level: no Lt entry, the gather skips it)
@@ -317,10 +344,10 @@ __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t
         const uint32_t mid = (lo + hi) >> 1;
         if (pre[mid] <= r) lo = mid; else hi = mid;
       }
-      const uint2 rec = a.area[(size_t)(c0 + lo) * a.PW * a.fc + sb[lo] + (r - pre[lo])];
-      uint32_t ql = rec.x - q0;
+      const RT rec = reinterpret_cast<const RT*>(a.area)[(size_t)(c0 + lo) * a.PW * a.fc + sb[lo] + (r - pre[lo])];
+      uint32_t ql = R::area_ql(rec, q0);
       if (GS_OOB(ql, BP, a.err, "binned record pair")) ql = 0;
-      if (pool_ok) a.pool[pbase + done + r] = make_uint2(ql, rec_hop | rec.y);
+      if (pool_ok) reinterpret_cast<RT*>(a.pool)[pbase + done + r] = R::pool(ql, rec_hop, R::area_src(rec));
       atomicOr(&vis[ql >> 5], 1u << (ql & 31));
     }
     done += ct;
@@ -358,7 +385,10 @@ __host__ __device__ inline size_t bin_gather_lds_bytes(uint32_t BS, uint32_t csr
 // After the last level: the binned levels' records of the bin go to inbound slots after
 // the direct levels' (cnt[pair] so far), rows written coalesced from an LDS CSR; cnt[pair]
 // becomes the round's in-degree.
+template <class R>
 __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
+  using RT = typename R::T;
+  const RT* pool = reinterpret_cast<const RT*>(a.pool);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t b = xcd_bin(blockIdx.x, a.nbins);
   if (b >= a.nbins) return;
@@ -378,7 +408,7 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
   for (uint32_t d = 0; d < 255 && a.lvl[d]; ++d) {
     if (a.lvl[d] < a.qmin) continue;
     const uint2 L = a.Lt[(size_t)d * nb + b];
-    for (uint32_t r = tid; r < L.y; r += GATHER_THREADS) atomicAdd(&cb[a.pool[L.x + r].x], 1u);
+    for (uint32_t r = tid; r < L.y; r += GATHER_THREADS) atomicAdd(&cb[R::pool_ql(pool[L.x + r])], 1u);
   }
   __syncthreads();
   uint32_t kmax = 0;
@@ -404,9 +434,10 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
     for (uint32_t d = 0; d < 255 && a.lvl[d]; ++d) {
       if (a.lvl[d] < a.qmin) continue;
       const uint2 L = a.Lt[(size_t)d * nb + b];
+      const uint32_t hopv = (d + 1) << 24;
       for (uint32_t r = tid; r < L.y; r += GATHER_THREADS) {
-        const uint2 rec = a.pool[L.x + r];
-        csr[atomicAdd(&of[rec.x], 1u)] = rec.y;
+        const RT rec = pool[L.x + r];
+        csr[atomicAdd(&of[R::pool_ql(rec)], 1u)] = R::pool_val(rec, hopv);
       }
     }
     __syncthreads();  // of[i] is now the END of pair i's list
@@ -422,10 +453,12 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
     for (uint32_t d = 0; d < 255 && a.lvl[d]; ++d) {
       if (a.lvl[d] < a.qmin) continue;
       const uint2 L = a.Lt[(size_t)d * nb + b];
+      const uint32_t hopv = (d + 1) << 24;
       for (uint32_t r = tid; r < L.y; r += GATHER_THREADS) {
-        const uint2 rec = a.pool[L.x + r];
-        const uint32_t k = atomicAdd(&of[rec.x], 1u);
-        if (k < a.capin) a.inb[(size_t)k * a.PAIRS + q0 + rec.x] = rec.y;
+        const RT rec = pool[L.x + r];
+        const uint32_t ql = R::pool_ql(rec);
+        const uint32_t k = atomicAdd(&of[ql], 1u);
+        if (k < a.capin) a.inb[(size_t)k * a.PAIRS + q0 + ql] = R::pool_val(rec, hopv);
       }
     }
   }
@@ -474,24 +507,63 @@ hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* coun
   return hipGetLastError();
 }
 
-void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g) {
+void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g, bool allow_narrow) {
   uint32_t lg = 0;
   while ((1ull << lg) < PAIRS) ++lg;
   g.BS = std::min(13u, std::max(11u, lg > 13 ? lg - 13 : 0u));  // <= 8192 bins up to 2^26 pairs
   g.nbins = (uint32_t)((PAIRS + (1ull << g.BS) - 1) >> g.BS);
-  uint32_t pw = 1024;
-  while (pw > 256 && (size_t)pw * fcap * 8 > 48 * 1024) pw >>= 1;  // LDS-staged records <= 48 KiB
+  g.narrow = allow_narrow && g.BS == NARROW_BS && N <= (1u << NARROW_SRC_BITS);
+  const uint32_t rb = g.narrow ? 4 : 8;
+  uint32_t pw = 2048;
+  while (pw > 256 && (size_t)pw * fcap * rb > 48 * 1024) pw >>= 1;  // LDS-staged records <= 48 KiB
   g.PW = pw;
   g.Gmax = (uint32_t)((PAIRS + pw - 1) / pw);
   g.T_words = (size_t)g.Gmax * (g.nbins + 1);
   // two gather workgroups per CU (LDS <= 80 KiB) for bins of 2^11 pairs, one beyond
   const size_t budget = g.BS <= 11 ? 80 * 1024 : 160 * 1024;
   g.csr_cap = (uint32_t)((budget - 4 * (3 * ((size_t)1 << g.BS) + 32)) / 4);
-  (void)N;
 }
 
 bool bin_supported(const BinGeom& g, uint32_t fcap) {
-  return g.T_words * 4 <= (1ull << 30) && bin_expand_lds_bytes(g.nbins, g.PW, fcap) <= 160 * 1024;
+  return g.T_words * 4 <= (1ull << 30) && bin_expand_lds_bytes(g.nbins, g.PW, fcap, g.narrow ? 4 : 8) <= 160 * 1024;
+}
+
+template <class R>
+static hipError_t run_binned(Engine& e, BinArgs& a) {
+  hipError_t r;
+  const size_t lds_x = bin_expand_lds_bytes(a.nbins, a.PW, a.fc, sizeof(typename R::T));
+  const size_t lds_a = bin_apply_lds_bytes(a.BS);
+  const size_t lds_g = bin_gather_lds_bytes(a.BS, a.csr_cap);
+  const uint32_t xth = a.PW / X_PPT;
+  const uint32_t xgrid = std::min<uint32_t>(a.Gmax, 256 * (xth <= 256 ? 2 : 1));  // slices looped
+  const uint32_t bgrid = ((a.nbins + 7) / 8) * 8;
+  const uint32_t dgrid = (uint32_t)std::min<size_t>(BIN_MIN_FRONTIER / 256, (e.PAIRS + 255) / 256);
+  if ((r = hipFuncSetAttribute((const void*)k_bin_apply<R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a)))
+    return r;
+  if ((r = hipFuncSetAttribute((const void*)k_bin_gather<R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
+    return r;
+  GS_ASZP_DISPATCH(e.ASZP, {
+    r = hipFuncSetAttribute((const void*)k_bin_expand<A, R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
+  });
+  if (r != hipSuccess) return r;
+  for (uint32_t d = 0; d < 254; ++d) {
+    if (a.qmin > 1)
+      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_bin_direct<A>, dim3(dgrid), dim3(256), 0, e.st, a, d,
+                                                  e.q[d & 1], e.q[(d + 1) & 1]));
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_expand<A, R>), dim3(xgrid), dim3(xth), lds_x, e.st, a, d,
+                                                e.q[d & 1]));
+    hipLaunchKernelGGL(k_bin_apply<R>, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
+    if ((d & 3) == 3) {  // poll the frontier size every 4 levels
+      uint32_t* h = e.h_err + 1;
+      if ((r = hipMemcpyAsync(h, e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st)) != hipSuccess) return r;
+      if ((r = hipStreamSynchronize(e.st)) != hipSuccess) return r;
+      if (*h == 0) {
+        hipLaunchKernelGGL(k_bin_gather<R>, dim3(bgrid), dim3(GATHER_THREADS), lds_g, e.st, a);
+        return hipGetLastError();
+      }
+    }
+  }
+  return hipErrorNotSupported;  // frontier still non-empty after 254 levels: hop counts no longer fit u8
 }
 
 hipError_t launch_bfs_binned(Engine& e, bool record) {
@@ -511,39 +583,7 @@ hipError_t launch_bfs_binned(Engine& e, bool record) {
   if ((r = hipMemsetAsync(e.cnt, 0, e.PAIRS * 4, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.bin_vis, 0, (e.PAIRS + 31) / 32 * 4, e.st)) != hipSuccess) return r;
   hipLaunchKernelGGL(k_bin_seed, dim3((e.S + 255) / 256), dim3(256), 0, e.st, a, e.origin, e.S, e.q[0]);
-  const size_t lds_x = bin_expand_lds_bytes(a.nbins, a.PW, a.fc);
-  const size_t lds_a = bin_apply_lds_bytes(a.BS);
-  const size_t lds_g = bin_gather_lds_bytes(a.BS, a.csr_cap);
-  const uint32_t xth = a.PW / X_PPT;
-  const uint32_t xgrid = std::min<uint32_t>(a.Gmax, 512);  // slices looped: empty levels cost one wave of workgroups
-  const uint32_t bgrid = ((a.nbins + 7) / 8) * 8;
-  const uint32_t dgrid = (uint32_t)std::min<size_t>(BIN_MIN_FRONTIER / 256, (e.PAIRS + 255) / 256);
-  if ((r = hipFuncSetAttribute((const void*)k_bin_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a)))
-    return r;
-  if ((r = hipFuncSetAttribute((const void*)k_bin_gather, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
-    return r;
-  GS_ASZP_DISPATCH(e.ASZP, {
-    r = hipFuncSetAttribute((const void*)k_bin_expand<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
-  });
-  if (r != hipSuccess) return r;
-  for (uint32_t d = 0; d < 254; ++d) {
-    if (a.qmin > 1)
-      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_bin_direct<A>, dim3(dgrid), dim3(256), 0, e.st, a, d,
-                                                  e.q[d & 1], e.q[(d + 1) & 1]));
-    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_bin_expand<A>, dim3(xgrid), dim3(xth), lds_x, e.st, a, d,
-                                                e.q[d & 1]));
-    hipLaunchKernelGGL(k_bin_apply, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
-    if ((d & 3) == 3) {  // poll the frontier size every 4 levels
-      uint32_t* h = e.h_err + 1;
-      if ((r = hipMemcpyAsync(h, e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st)) != hipSuccess) return r;
-      if ((r = hipStreamSynchronize(e.st)) != hipSuccess) return r;
-      if (*h == 0) {
-        hipLaunchKernelGGL(k_bin_gather, dim3(bgrid), dim3(GATHER_THREADS), lds_g, e.st, a);
-        return hipGetLastError();
-      }
-    }
-  }
-  return hipErrorNotSupported;  // frontier still non-empty after 254 levels: hop counts no longer fit u8
+  return e.bin.narrow ? run_binned<RecN>(e, a) : run_binned<RecW>(e, a);
 }
 
 }  // namespace gs

@@ -172,7 +172,7 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   uint32_t mode = prm->bfs_mode;
   const size_t lds = bfs_wg_lds_bytes(n);
   const size_t pairs = (size_t)n * n_slots;
-  bin_geometry(n, pairs, e->fcap, e->bin);
+  bin_geometry(n, pairs, e->fcap, e->bin, !(prm->flags & GS_FLAG_WIDE_RECORDS));
   const bool bin_ok = pairs <= (1ull << 28) && bin_supported(e->bin, e->fcap);
   if (mode == GS_BFS_AUTO)
     mode = (n <= 8192 && n_slots >= 64) ? GS_BFS_WORKGROUP : (bin_ok ? GS_BFS_BINNED : GS_BFS_LEVEL);

@@ -25,6 +25,7 @@ namespace gs {
 struct BinGeom {
   uint32_t BS = 0, nbins = 0, PW = 0, Gmax = 0, csr_cap = 0;
   size_t T_words = 0;
+  bool narrow = false;  // 4-byte records (bins of 2^11 pairs, N <= 2^21)
 };
 
 struct Engine {
@@ -152,7 +153,7 @@ hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket, ui
 hipError_t launch_bfs(Engine& e, bool record);
 hipError_t launch_bfs_binned(Engine& e, bool record);
 hipError_t launch_bfs_level_step(Engine& e, bool record, uint32_t d, uint32_t qmin, uint32_t qmax);
-void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g);
+void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g, bool allow_narrow);
 bool bin_supported(const BinGeom& g, uint32_t fcap);
 // own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);

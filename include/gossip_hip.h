@@ -52,7 +52,8 @@ enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24
  * propagation-blocked (pushes binned by destination range, LDS counters per
  * bin; large clusters). AUTO picks WORKGROUP, else BINNED, else LEVEL. */
 enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2, GS_BFS_BINNED = 3 };
-enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4, GS_FLAG_BINNED_ALL_LEVELS = 8 };
+enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4, GS_FLAG_BINNED_ALL_LEVELS = 8,
+       GS_FLAG_WIDE_RECORDS = 16 };
 
 typedef struct gs_params {
   uint32_t push_fanout;         /* Config::gossip_push_fanout (gossip.rs:113) */
@@ -71,7 +72,9 @@ typedef struct gs_params {
                                    <= 4 (not 16) and the wave consume for in-degree <= 8 (not 64)
                                    (same results; lets small test clusters cover every path);
                                    GS_FLAG_BINNED_ALL_LEVELS: GS_BFS_BINNED bins every level, not
-                                   only levels with >= 2^17 frontier pairs (same results) */
+                                   only levels with >= 2^17 frontier pairs (same results);
+                                   GS_FLAG_WIDE_RECORDS: GS_BFS_BINNED keeps 8-byte push records
+                                   even where 4-byte ones fit (same results) */
 } gs_params;
 
 typedef struct gs_slot {

@@ -25,7 +25,7 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
   # HBM traffic of the round kernel over the bench's own default timed steps (separate passes)
-  BENCH_ARGS="--steps 100 --warmup 20 --no-cpu-baseline --no-profile" bash scripts/pmc.sh fetch:FETCH_SIZE write:WRITE_SIZE || exit $?
+  BENCH_ARGS="--steps 100 --warmup 20 --no-cpu-baseline --no-profile --no-large" bash scripts/pmc.sh fetch:FETCH_SIZE write:WRITE_SIZE || exit $?
   python3 scripts/pmc_summary.py --kernel k_round_wg --launches 100 --bench-args "--steps 100 --warmup 20" \
     --out gpurun_out/pmc_k_round_wg_3000x3000.json && mkdir -p $ROUND_DIR && \
     cp gpurun_out/pmc_k_round_wg_3000x3000.json $ROUND_DIR/

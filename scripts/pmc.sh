@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-ARGS=${BENCH_ARGS:-"--steps 20 --warmup 22 --no-cpu-baseline --no-profile"}
+ARGS=${BENCH_ARGS:-"--steps 20 --warmup 22 --no-cpu-baseline --no-profile --no-large"}
 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
 run() {  # run <tag> <counters...>
   local tag=$1; shift

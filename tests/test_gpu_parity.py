@@ -353,16 +353,17 @@ def test_large_network_invariants():
         assert (dest >= 0).all()
 
 
-@pytest.mark.parametrize("all_levels", [False, True])
-def test_binned_bfs_matches_level_bfs_large(all_levels):
+@pytest.mark.parametrize("all_levels,wide", [(False, False), (True, False), (True, True)])
+def test_binned_bfs_matches_level_bfs_large(all_levels, wide):
     """N = 300k, 3 slots, a fail-nodes fraction: the propagation-blocked BFS (hybrid
-    with the level kernel for small levels, or binned throughout) gives the level
-    BFS's hops, in-degrees, inbound sets, counters and summaries."""
+    with the direct kernel for small levels, or binned throughout; 4- or 8-byte
+    records) gives the level BFS's hops, in-degrees, inbound sets, counters and
+    summaries."""
     n = 300_000
     st = eb.synth.power_law_stakes(n)
     engs = [gs.Engine(st, 3, seed=33, rotation_probability=0.01, bfs_mode=gs.GS_BFS_LEVEL),
             gs.Engine(st, 3, seed=33, rotation_probability=0.01, bfs_mode=gs.GS_BFS_BINNED,
-                      binned_all_levels=all_levels)]
+                      binned_all_levels=all_levels, wide_records=wide)]
     for e in engs:
         e.set_slots([0, 17, n - 1], [2, 1, 3], [0.15, 0.3, 0.05])
         e.init_active_sets()
