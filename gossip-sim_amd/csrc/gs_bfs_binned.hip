@@ -147,12 +147,76 @@ __host__ __device__ inline size_t bin_expand_lds_bytes(uint32_t nbins, uint32_t 
   return 4 * (size_t)((nbins + 16 + 1) & ~1u) + rec_bytes * (size_t)PW * fc;
 }
 
+// Levels with fewer than qmin (BIN_MIN_FRONTIER) frontier pairs: one thread per frontier pair,
+// a global in-degree atomic per push (cheap when there are few) that also gives the
+// record's inbound slot; first visits from the round's visited bitmap, shared with the
+// binned levels. The gather places the binned levels' records after these slots.
+constexpr uint32_t BIN_MIN_FRONTIER = 1u << 17;
+
+template <int ASZP>
+__device__ inline void bin_direct(const BinArgs& a, uint32_t d, uint32_t qn, const uint32_t* __restrict__ qcur,
+                                  uint32_t* __restrict__ qnxt) {
+  const uint32_t rec_hop = (d + 1) << 24;
+  bool overflow = false;
+  for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < qn; i0 += gridDim.x * blockDim.x) {  // uniform trips
+    const uint32_t i = i0 + threadIdx.x;
+    uint32_t row[ASZP], pm = 0, o = 0, u = 0;
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) row[s] = 0;
+    if (i < qn) {
+      uint32_t p = qcur[i];
+      if (GS_OOB(p, a.PAIRS, a.err, "direct frontier pair")) p = 0;
+      pm = pair_pushes<ASZP>(a, p, row, o, u);
+      const uint32_t eg = __popc(pm);
+      a.egress[p] = (uint8_t)eg;
+      if (a.record && eg) a.egress_acc[p] += eg;
+    }
+    const uint32_t qb = o * a.N;
+    uint32_t slot[ASZP], vold[ASZP];
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) {  // all atomics back to back, then their results
+      const uint32_t q = qb + row[s];
+      const bool on = (pm >> s) & 1u;
+      slot[s] = on ? atomicAdd(&a.cnt[q], 1u) : 0u;
+      vold[s] = on ? atomicOr(&a.visbm[q >> 5], 1u << (q & 31)) : ~0u;
+    }
+    uint32_t newm = 0;
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) {
+      if (!((pm >> s) & 1u)) continue;
+      const uint32_t q = qb + row[s];
+      if (slot[s] < a.capin) a.inb[(size_t)slot[s] * a.PAIRS + q] = rec_hop | u;
+      else overflow = true;
+      if (!((vold[s] >> (q & 31)) & 1u)) {  // first visit: hop = dist[src] + 1 (gossip.rs:594-600)
+        newm |= 1u << s;
+        a.hops[q] = (uint8_t)(d + 1);
+      }
+    }
+    const uint32_t k = __popc(newm);
+    const uint32_t incl = wave_incl_scan(k);
+    const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+    uint32_t qbase = 0;
+    if (lane_id() == 63 && tot) qbase = atomicAdd(&a.lvl[d + 1], tot);
+    uint32_t pos = (uint32_t)__shfl((int)qbase, 63) + incl - k;
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s)
+      if ((newm >> s) & 1u) qnxt[pos++] = qb + row[s];
+  }
+  if (overflow) atomicOr(a.err, ERR_INBOUND);
+}
+
+// A level with fewer than qmin frontier pairs runs bin_direct in this same launch
+// (no dispatch of its own); a larger one is expanded into bin runs for k_bin_apply.
 template <int ASZP, class R>
-__global__ __launch_bounds__(512) void k_bin_expand(BinArgs a, uint32_t d, const uint32_t* __restrict__ qcur) {
+__global__ __launch_bounds__(512) void k_bin_expand(BinArgs a, uint32_t d, const uint32_t* __restrict__ qcur,
+                                                    uint32_t* __restrict__ qnxt) {
   using RT = typename R::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t qn = a.lvl[d];
-  if (qn < a.qmin) return;  // k_bin_direct's level
+  if (qn < a.qmin) {
+    bin_direct<ASZP>(a, d, qn, qcur, qnxt);
+    return;
+  }
   const uint32_t G = (qn + a.PW - 1) / a.PW;
   const uint32_t nb = a.nbins, BS = a.BS, tid = threadIdx.x, TH = blockDim.x;
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);                               // [nb] + 16
@@ -208,66 +272,6 @@ __global__ __launch_bounds__(512) void k_bin_expand(BinArgs a, uint32_t d, const
   }
 }
 
-// Levels with fewer than BIN_MIN_FRONTIER frontier pairs: one thread per frontier pair,
-// a global in-degree atomic per push (cheap when there are few) that also gives the
-// record's inbound slot; first visits from the round's visited bitmap, shared with the
-// binned levels. The gather places the binned levels' records after these slots.
-constexpr uint32_t BIN_MIN_FRONTIER = 1u << 17;
-
-template <int ASZP>
-__global__ __launch_bounds__(256) void k_bin_direct(BinArgs a, uint32_t d, const uint32_t* __restrict__ qcur,
-                                                   uint32_t* __restrict__ qnxt) {
-  const uint32_t qn = a.lvl[d];
-  if (qn >= a.qmin) return;
-  const uint32_t rec_hop = (d + 1) << 24;
-  bool overflow = false;
-  for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < qn; i0 += gridDim.x * blockDim.x) {  // uniform trips
-    const uint32_t i = i0 + threadIdx.x;
-    uint32_t row[ASZP], pm = 0, o = 0, u = 0;
-#pragma unroll
-    for (int s = 0; s < ASZP; ++s) row[s] = 0;
-    if (i < qn) {
-      uint32_t p = qcur[i];
-      if (GS_OOB(p, a.PAIRS, a.err, "direct frontier pair")) p = 0;
-      pm = pair_pushes<ASZP>(a, p, row, o, u);
-      const uint32_t eg = __popc(pm);
-      a.egress[p] = (uint8_t)eg;
-      if (a.record && eg) a.egress_acc[p] += eg;
-    }
-    const uint32_t qb = o * a.N;
-    uint32_t slot[ASZP], vold[ASZP];
-#pragma unroll
-    for (int s = 0; s < ASZP; ++s) {  // all atomics back to back, then their results
-      const uint32_t q = qb + row[s];
-      const bool on = (pm >> s) & 1u;
-      slot[s] = on ? atomicAdd(&a.cnt[q], 1u) : 0u;
-      vold[s] = on ? atomicOr(&a.visbm[q >> 5], 1u << (q & 31)) : ~0u;
-    }
-    uint32_t newm = 0;
-#pragma unroll
-    for (int s = 0; s < ASZP; ++s) {
-      if (!((pm >> s) & 1u)) continue;
-      const uint32_t q = qb + row[s];
-      if (slot[s] < a.capin) a.inb[(size_t)slot[s] * a.PAIRS + q] = rec_hop | u;
-      else overflow = true;
-      if (!((vold[s] >> (q & 31)) & 1u)) {  // first visit: hop = dist[src] + 1 (gossip.rs:594-600)
-        newm |= 1u << s;
-        a.hops[q] = (uint8_t)(d + 1);
-      }
-    }
-    const uint32_t k = __popc(newm);
-    const uint32_t incl = wave_incl_scan(k);
-    const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
-    uint32_t qbase = 0;
-    if (lane_id() == 63 && tot) qbase = atomicAdd(&a.lvl[d + 1], tot);
-    uint32_t pos = (uint32_t)__shfl((int)qbase, 63) + incl - k;
-#pragma unroll
-    for (int s = 0; s < ASZP; ++s)
-      if ((newm >> s) & 1u) qnxt[pos++] = qb + row[s];
-  }
-  if (overflow) atomicOr(a.err, ERR_INBOUND);
-}
-
 // apply LDS: pre [SEG_CHUNK + 1], sb [SEG_CHUNK], vis / vis0 bitmaps [BP / 32], control
 __host__ __device__ inline size_t bin_apply_lds_bytes(uint32_t BS) {
   return 4 * (2 * (size_t)SEG_CHUNK + 1 + 2 * (((size_t)1 << BS) / 32) + 32);
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t
   using RT = typename R::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t qn = a.lvl[d];
-  if (qn == 0 || qn < a.qmin) return;  // (k_bin_direct's level: no Lt entry, the gather skips it)
+  if (qn == 0 || qn < a.qmin) return;  // (a direct level: no Lt entry, the gather skips it)
   const uint32_t b = xcd_bin(blockIdx.x, a.nbins);
   if (b >= a.nbins) return;
   const uint32_t tid = threadIdx.x, nb = a.nbins, BP = 1u << a.BS, NW = BP / 32;
@@ -537,7 +541,6 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
   const uint32_t xth = a.PW / X_PPT;
   const uint32_t xgrid = std::min<uint32_t>(a.Gmax, 256 * (xth <= 256 ? 2 : 1));  // slices looped
   const uint32_t bgrid = ((a.nbins + 7) / 8) * 8;
-  const uint32_t dgrid = (uint32_t)std::min<size_t>(BIN_MIN_FRONTIER / 256, (e.PAIRS + 255) / 256);
   if ((r = hipFuncSetAttribute((const void*)k_bin_apply<R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a)))
     return r;
   if ((r = hipFuncSetAttribute((const void*)k_bin_gather<R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
@@ -547,13 +550,12 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
   });
   if (r != hipSuccess) return r;
   for (uint32_t d = 0; d < 254; ++d) {
-    if (a.qmin > 1)
-      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_bin_direct<A>, dim3(dgrid), dim3(256), 0, e.st, a, d,
-                                                  e.q[d & 1], e.q[(d + 1) & 1]));
     GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_expand<A, R>), dim3(xgrid), dim3(xth), lds_x, e.st, a, d,
-                                                e.q[d & 1]));
+                                                e.q[d & 1], e.q[(d + 1) & 1]));
     hipLaunchKernelGGL(k_bin_apply<R>, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
-    if ((d & 3) == 3) {  // poll the frontier size every 4 levels
+    // poll the frontier size after 12 levels, then every 4: a poll idles the GPU for a
+    // host round trip (~35 us), an empty level costs two no-op dispatches (~7 us)
+    if (d >= 11 && (d & 3) == 3) {
       uint32_t* h = e.h_err + 1;
       if ((r = hipMemcpyAsync(h, e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st)) != hipSuccess) return r;
       if ((r = hipStreamSynchronize(e.st)) != hipSuccess) return r;
