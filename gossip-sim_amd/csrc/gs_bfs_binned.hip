@@ -381,19 +381,23 @@ __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t
   }
 }
 
-// gather LDS: direct-level in-degrees [BP], binned counts [BP], CSR cursors [BP], CSR [csr_cap]
+// gather LDS: direct-level in-degrees [BP], binned counts [BP], CSR cursors [BP], CSR [csr_cap],
+// per-level run table [3][256] + prefix [257], scan words
+constexpr uint32_t G_CACHE = 24;  // pool records per thread kept in registers between the passes
 __host__ __device__ inline size_t bin_gather_lds_bytes(uint32_t BS, uint32_t csr_cap) {
-  return 4 * (3 * ((size_t)1 << BS) + (size_t)csr_cap + 32);
+  return 4 * (3 * ((size_t)1 << BS) + (size_t)csr_cap + 3 * 256 + 257 + 32);
 }
 
 // After the last level: the binned levels' records of the bin go to inbound slots after
 // the direct levels' (cnt[pair] so far), rows written coalesced from an LDS CSR; cnt[pair]
-// becomes the round's in-degree.
+// becomes the round's in-degree. Records are numbered f over the bin's level runs in
+// level order; a thread takes f = tid + j * GATHER_THREADS and keeps its first G_CACHE
+// records in registers for the placement pass.
 template <class R>
 __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
   using RT = typename R::T;
-  const RT* pool = reinterpret_cast<const RT*>(a.pool);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const RT* pool = reinterpret_cast<const RT*>(a.pool);
   const uint32_t b = xcd_bin(blockIdx.x, a.nbins);
   if (b >= a.nbins) return;
   const uint32_t tid = threadIdx.x, nb = a.nbins, BP = 1u << a.BS;
@@ -401,18 +405,51 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
   uint32_t* cb = cd + BP;                            // [BP] binned-level records
   uint32_t* of = cb + BP;                            // [BP] CSR cursor
   uint32_t* csr = of + BP;                           // [csr_cap]
-  uint32_t* ctl = csr + a.csr_cap;                   // scan words
+  uint32_t* rs = csr + a.csr_cap;                    // [256] pool start of level d's run
+  uint32_t* rp = rs + 256;                           // [257] records before level d's run
+  uint32_t* ctl = rp + 257;                          // scan words
   const uint32_t q0 = b << a.BS;
   const uint32_t nq = (uint32_t)min((size_t)BP, a.PAIRS - q0);
   for (uint32_t i = tid; i < BP; i += GATHER_THREADS) {
     cd[i] = i < nq ? a.cnt[q0 + i] : 0u;
     cb[i] = 0;
   }
+  uint32_t rn = 0;  // 1. run table: thread d < 255 reads level d's run
+  if (tid < 255) {
+    const uint32_t q = a.lvl[tid];
+    if (q >= a.qmin && q) {
+      const uint2 L = a.Lt[(size_t)tid * nb + b];
+      rs[tid] = L.x;
+      rn = L.y;
+    }
+  }
+  {
+    const uint32_t incl = wave_incl_scan(rn);
+    if ((tid & 63) == 63) ctl[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t off = incl - rn;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) off += ctl[w];
+    if (tid < 256) rp[tid] = off;
+    if (tid == 255) rp[256] = off + rn;
+  }
   __syncthreads();
-  for (uint32_t d = 0; d < 255 && a.lvl[d]; ++d) {
-    if (a.lvl[d] < a.qmin) continue;
-    const uint2 L = a.Lt[(size_t)d * nb + b];
-    for (uint32_t r = tid; r < L.y; r += GATHER_THREADS) atomicAdd(&cb[R::pool_ql(pool[L.x + r])], 1u);
+  const uint32_t Etot = rp[256];
+  if (Etot == 0) return;  // no binned-level records: cnt[] already holds the in-degrees
+  // 2. count per pair; cache records
+  RT cache[G_CACHE];
+  uint32_t lv = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < G_CACHE; ++j) {
+    const uint32_t f = tid + j * GATHER_THREADS;
+    if (f < Etot) {
+      while (f >= rp[lv + 1]) ++lv;
+      cache[j] = pool[rs[lv] + (f - rp[lv])];
+      atomicAdd(&cb[R::pool_ql(cache[j])], 1u);
+    }
+  }
+  for (uint32_t f = tid + G_CACHE * GATHER_THREADS; f < Etot; f += GATHER_THREADS) {
+    while (f >= rp[lv + 1]) ++lv;
+    atomicAdd(&cb[R::pool_ql(pool[rs[lv] + (f - rp[lv])])], 1u);
   }
   __syncthreads();
   uint32_t kmax = 0;
@@ -432,39 +469,52 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
   __syncthreads();
   kmax = 0;
   for (uint32_t k = 0; k < GATHER_THREADS / 64; ++k) kmax = max(kmax, ctl[16 + k]);
-  if (kmax == 0) return;
   const uint32_t E = block_excl_scan(of, BP, ctl);  // of[i] = CSR start of pair i
-  if (E <= a.csr_cap) {
-    for (uint32_t d = 0; d < 255 && a.lvl[d]; ++d) {
-      if (a.lvl[d] < a.qmin) continue;
-      const uint2 L = a.Lt[(size_t)d * nb + b];
-      const uint32_t hopv = (d + 1) << 24;
-      for (uint32_t r = tid; r < L.y; r += GATHER_THREADS) {
-        const RT rec = pool[L.x + r];
-        csr[atomicAdd(&of[R::pool_ql(rec)], 1u)] = R::pool_val(rec, hopv);
-      }
-    }
-    __syncthreads();  // of[i] is now the END of pair i's list
-    for (uint32_t k = 0; k < kmax; ++k)
-      for (uint32_t i = tid; i < nq; i += GATHER_THREADS) {
-        const uint32_t c = cb[i], slot = cd[i] + k;
-        if (k < c && slot < a.capin) a.inb[(size_t)slot * a.PAIRS + q0 + i] = csr[of[i] - c + k];
-      }
-  } else {  // more records than the LDS CSR holds: place each one directly
-    __syncthreads();
+  const bool in_lds = E <= a.csr_cap;
+  if (!in_lds) {  // more records than the LDS CSR holds: cursors at the direct count, placed directly
     for (uint32_t i = tid; i < BP; i += GATHER_THREADS) of[i] = cd[i];
     __syncthreads();
-    for (uint32_t d = 0; d < 255 && a.lvl[d]; ++d) {
-      if (a.lvl[d] < a.qmin) continue;
-      const uint2 L = a.Lt[(size_t)d * nb + b];
-      const uint32_t hopv = (d + 1) << 24;
-      for (uint32_t r = tid; r < L.y; r += GATHER_THREADS) {
-        const RT rec = pool[L.x + r];
-        const uint32_t ql = R::pool_ql(rec);
-        const uint32_t k = atomicAdd(&of[ql], 1u);
-        if (k < a.capin) a.inb[(size_t)k * a.PAIRS + q0 + ql] = R::pool_val(rec, hopv);
-      }
+  }
+  // 3. placement (cached records first, then re-read ones)
+  lv = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < G_CACHE; ++j) {
+    const uint32_t f = tid + j * GATHER_THREADS;
+    if (f < Etot) {
+      while (f >= rp[lv + 1]) ++lv;
+      const uint32_t ql = R::pool_ql(cache[j]), v = R::pool_val(cache[j], (lv + 1) << 24);
+      const uint32_t pos = atomicAdd(&of[ql], 1u);
+      if (in_lds) csr[pos] = v;
+      else if (pos < a.capin) a.inb[(size_t)pos * a.PAIRS + q0 + ql] = v;
     }
+  }
+  for (uint32_t f = tid + G_CACHE * GATHER_THREADS; f < Etot; f += GATHER_THREADS) {
+    while (f >= rp[lv + 1]) ++lv;
+    const RT rec = pool[rs[lv] + (f - rp[lv])];
+    const uint32_t ql = R::pool_ql(rec), v = R::pool_val(rec, (lv + 1) << 24);
+    const uint32_t pos = atomicAdd(&of[ql], 1u);
+    if (in_lds) csr[pos] = v;
+    else if (pos < a.capin) a.inb[(size_t)pos * a.PAIRS + q0 + ql] = v;
+  }
+  if (!in_lds) return;
+  __syncthreads();  // of[i] is now the END of pair i's list
+  // 4. rows k of the bin, coalesced over pairs; per-pair state hoisted out of the k loop
+  constexpr uint32_t PPT = 4;  // BP / GATHER_THREADS pairs per thread (BP <= 2048 here; more loop below)
+  for (uint32_t i0 = 0; i0 < nq; i0 += PPT * GATHER_THREADS) {
+    uint32_t c[PPT], st[PPT], sl[PPT];
+#pragma unroll
+    for (uint32_t t = 0; t < PPT; ++t) {
+      const uint32_t i = i0 + t * GATHER_THREADS + tid;
+      c[t] = i < nq ? cb[i] : 0u;
+      st[t] = i < nq ? of[i] - c[t] : 0u;
+      sl[t] = i < nq ? cd[i] : 0u;
+    }
+    for (uint32_t k = 0; k < kmax; ++k)
+#pragma unroll
+      for (uint32_t t = 0; t < PPT; ++t) {
+        const uint32_t i = i0 + t * GATHER_THREADS + tid;
+        if (k < c[t] && sl[t] + k < a.capin) a.inb[(size_t)(sl[t] + k) * a.PAIRS + q0 + i] = csr[st[t] + k];
+      }
   }
 }
 
@@ -525,7 +575,7 @@ void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g, bool allo
   g.T_words = (size_t)g.Gmax * (g.nbins + 1);
   // two gather workgroups per CU (LDS <= 80 KiB) for bins of 2^11 pairs, one beyond
   const size_t budget = g.BS <= 11 ? 80 * 1024 : 160 * 1024;
-  g.csr_cap = (uint32_t)((budget - 4 * (3 * ((size_t)1 << g.BS) + 32)) / 4);
+  g.csr_cap = (uint32_t)((budget - 4 * (3 * ((size_t)1 << g.BS) + 3 * 256 + 257 + 32)) / 4);
 }
 
 bool bin_supported(const BinGeom& g, uint32_t fcap) {
