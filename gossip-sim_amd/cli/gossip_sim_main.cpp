@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -38,7 +39,7 @@ const char* F64_NAMES[] = {"coverage", "rmr", "branching", "hop_mean", "hop_medi
 const char* U64_NAMES[] = {"origin", "hop_max", "hop_min", "aggregate_hops", "ldh", "stranded", "stranded_times",
                            "stranded_round_count", "stranded_round_max", "stranded_round_min", "hops_hist",
                            "stranded_hist", "egress_hist", "ingress_hist", "prune_hist", "egress_cpb",
-                           "validator_hist", "hist_errors", "failed_count"};
+                           "validator_hist", "hist_errors", "failed_count", "rmr_m", "rmr_n"};
 
 [[noreturn]] void die(int code, const std::string& msg) {
   std::fprintf(stderr, "error: %s\n", msg.c_str());
@@ -69,6 +70,8 @@ struct Cli {
   // engine / offline extensions
   uint64_t synthetic = 0, seed = 0x5EED0003ull, gpus = 1, bfs_mode = GS_BFS_AUTO;
   std::string save_results, replay_results;
+  std::string influx_file;  // offline Influx line protocol (gs_influx.cpp)
+  uint64_t influx_time_base = 0;
 };
 
 void usage() {
@@ -89,6 +92,8 @@ void usage() {
       "  --synthetic N        the deterministic synthetic power-law network of N nodes instead of RPC\n"
       "  --seed S [0x5EED0003] --gpus K [1] --bfs-mode 0..3 [0 = auto]\n"
       "  --save-results PATH  --replay-results PATH (print the report of a saved run, no GPU)\n"
+      "  --influx-file PATH   write the Influx series (influx_db.rs) as line protocol to PATH\n"
+      "  --influx-time-base NS  reproducible Influx timestamps NS + 1000 k (default: wall clock)\n"
       "gossip-sim write-accounts --account-file PATH --synthetic N [--num-nodes K] [--zero-stakes] [-f]");
 }
 
@@ -157,6 +162,8 @@ Cli parse(int argc, char** argv) {
     else if (a == "--bfs-mode") u64(i, c.bfs_mode);
     else if (a == "--save-results") c.save_results = need(i);
     else if (a == "--replay-results") c.replay_results = need(i);
+    else if (a == "--influx-file") c.influx_file = need(i);
+    else if (a == "--influx-time-base") u64(i, c.influx_time_base);
     else die(2, "unexpected argument '" + a + "' (see --help)");
   }
   return c;
@@ -271,6 +278,8 @@ int write_accounts_main(int argc, char** argv) {
 int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "write-accounts") == 0) return write_accounts_main(argc, argv);
   const Cli c = parse(argc, argv);
+  const uint64_t start_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(  // gossip_main.rs:724
+                                std::chrono::system_clock::now().time_since_epoch()).count();
 
   // validators and value parsing of gossip_main.rs:120-148,248-252,655-704
   double p0 = 0, thr0 = 0, frac0 = 0;
@@ -432,6 +441,41 @@ int main(int argc, char** argv) {
   if (!c.save_results.empty()) {
     std::string err;
     if (!gsrep::save_results(c.save_results, sims, err)) die(1, err);
+  }
+  if (!c.influx_file.empty()) {  // the datapoint queue's text, in enqueue order (gossip_main.rs:372-645)
+    gsrep::ReportInput in;
+    in.keys = keys;
+    in.stakes = stakes;
+    in.iterations = c.iterations;
+    in.warm_up_rounds = c.warm_up;
+    in.num_simulations = num_sims;
+    in.test_type = test_type;
+    in.nb_stranded = c.nb_stranded;
+    in.nb_message = c.nb_message;
+    in.nb_hops = c.nb_hops;
+    in.params = params;
+    in.sims = sims;
+    gsrep::InfluxOptions io;
+    io.time_base = c.influx_time_base;
+    io.start_time = std::to_string(c.influx_time_base ? c.influx_time_base : start_ns);
+    io.api = c.accounts_from_yaml ? c.account_file : "synthetic:" + std::to_string(c.synthetic);
+    if (num_sims) {
+      const gsrep::SimParams& q = params[0];
+      switch (test_type) {
+        case gsrep::ACTIVE_SET_SIZE: io.start_value = (double)q.gossip_active_set_size; break;
+        case gsrep::PUSH_FANOUT: io.start_value = (double)c.fanout; break;
+        case gsrep::MIN_INGRESS_NODES: io.start_value = (double)q.min_ingress_nodes; break;
+        case gsrep::PRUNE_STAKE_THRESHOLD: io.start_value = q.prune_stake_threshold; break;
+        case gsrep::ORIGIN_RANK: io.start_value = (double)q.origin_rank; break;
+        case gsrep::FAIL_NODES: io.start_value = q.fraction_to_fail; break;
+        case gsrep::ROTATE_PROBABILITY: io.start_value = q.probability_of_rotation; break;
+        default: break;
+      }
+    }
+    FILE* f = std::fopen(c.influx_file.c_str(), "w");
+    if (!f) die(1, "cannot write " + c.influx_file);
+    gsrep::write_influx(f, in, io);
+    std::fclose(f);
   }
   if (c.print_stats) {
     // GossipStatsCollection holds only simulations that recorded rounds (gossip_main.rs:567-593)

@@ -65,6 +65,15 @@ void log_warn(FILE* out, const char* target, const std::string& msg);
 // GossipStatsCollection::print_all(gossip_iterations, warm_up_rounds, test_type).
 void print_all(FILE* out, const ReportInput& in);
 
+// The InfluxDB series of influx_db.rs as an offline line-protocol file (gs_influx.cpp).
+struct InfluxOptions {
+  std::string start_time;   // start_time tag: the run's start in ns (gossip_main.rs:724)
+  std::string api;          // simulation_config.api: where the accounts came from
+  double start_value = 0;   // simulation_config.start_value: the swept parameter of simulation 0
+  uint64_t time_base = 0;   // 0: wall clock; else timestamps base + 1000 * k (reproducible)
+};
+void write_influx(FILE* out, const ReportInput& in, const InfluxOptions& opt);
+
 // Result arrays as text: hex-float f64 (exact), decimal u64.
 bool save_results(const std::string& path, const std::vector<SimArrays>& sims, std::string& err);
 bool load_results(const std::string& path, std::vector<SimArrays>& sims, std::string& err);

@@ -245,12 +245,14 @@ int gs_run_simulations(const gs_sim_config* cfg, const uint64_t* stakes, uint32_
     CK(gs_read_accumulators(e, s, eg.data(), in.data(), pr.data(), st.data(), hh.data()));
     CK(gs_read_failed(e, s, failed.data()));
     std::vector<double> cov, rmr, br, hmean, hmed, smean, smed;
-    std::vector<uint64_t> hmax, hmin, scnt, smax, smin;
+    std::vector<uint64_t> hmax, hmin, scnt, smax, smin, rm, rn;
     for (uint32_t k = 0; k < rounds; ++k) {
       const gs_round_summary& q = sums[(size_t)k * n_sims + s];
       cov.push_back((double)q.visited / (double)n);
       const uint64_t m = (uint64_t)q.pushes + q.prunes;
       rmr.push_back((double)m / (double)(q.visited - 1) - 1.0);
+      rm.push_back(m);
+      rn.push_back(q.visited);
       br.push_back(q.visited ? (double)q.pushes / (double)q.visited : 0.0);
       // per-round HopsStat
       double mean = (double)q.hop_sum / (double)q.hop_count, med = 0.0;
@@ -272,6 +274,7 @@ int gs_run_simulations(const gs_sim_config* cfg, const uint64_t* stakes, uint32_
       }
     }
     o.f["coverage"] = cov; o.f["rmr"] = rmr; o.f["branching"] = br;
+    o.u["rmr_m"] = rm; o.u["rmr_n"] = rn;  // the rmr datapoint's m, n (influx_db.rs:346-360)
     o.f["hop_mean"] = hmean; o.f["hop_median"] = hmed;
     o.u["hop_max"] = hmax; o.u["hop_min"] = hmin;
     o.u["stranded_round_count"] = scnt; o.u["stranded_round_max"] = smax; o.u["stranded_round_min"] = smin;

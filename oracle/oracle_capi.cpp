@@ -439,6 +439,8 @@ size_t or_res_u64(void* hp, const char* name, uint64_t* out, size_t cap) {
     return put_u(v, out, cap);
   }
   if (n == "aggregate_hops") return put_u({st.aggregate_hops.max, st.aggregate_hops.min}, out, cap);
+  if (n == "rmr_m") return put_u(st.rmr_m, out, cap);
+  if (n == "rmr_n") return put_u(st.rmr_n, out, cap);
   if (n == "ldh") return put_u({st.ldh.max, st.ldh.min}, out, cap);
   if (n == "stranded_round_count" || n == "stranded_round_max" || n == "stranded_round_min") {
     std::vector<uint64_t> v;

@@ -441,7 +441,11 @@ void run_simulation(const SimConfig& cfg, const std::vector<Pubkey>& pks, const 
       stats.ingress.update(sim.cluster.ingress_message_count);
       stats.prune.update(sim.cluster.prune_messages_sent);
       double r; uint64_t m, n;
-      if (sim.cluster.relative_message_redundancy(&r, &m, &n)) stats.rmr.collection.push_back(r);
+      if (sim.cluster.relative_message_redundancy(&r, &m, &n)) {
+        stats.rmr.collection.push_back(r);
+        stats.rmr_m.push_back(m);
+        stats.rmr_n.push_back(n);
+      }
     }
   }
   if (!stats.coverage.collection.empty()) {

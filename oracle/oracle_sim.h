@@ -112,6 +112,7 @@ struct GossipStats {  // gossip_stats.rs:1228-1884
   HopsStat aggregate_hops, ldh;
   Histogram hops_histogram;
   StatCollection coverage, rmr, branching;
+  std::vector<uint64_t> rmr_m, rmr_n;  // per measured round: the (m, n) of the rmr datapoint (influx_db.rs:346-360)
   StrandedNodeCollection stranded;
   Tracker egress, ingress, prune;
   Histogram validator_stake_distribution;

@@ -15,6 +15,7 @@ import pytest
 
 import engine_bind as eb
 import oracle_bind as ob
+import influx_ref as ir
 import report_ref as rr
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -24,7 +25,7 @@ F64_NAMES = ["coverage", "rmr", "branching", "hop_mean", "hop_median", "coverage
 U64_NAMES = ["origin", "hop_max", "hop_min", "aggregate_hops", "ldh", "stranded", "stranded_times",
              "stranded_round_count", "stranded_round_max", "stranded_round_min", "hops_hist", "stranded_hist",
              "egress_hist", "ingress_hist", "prune_hist", "egress_cpb", "validator_hist", "hist_errors",
-             "failed_count"]
+             "failed_count", "rmr_m", "rmr_n"]
 
 
 def cli(*args, check=True):
@@ -161,6 +162,35 @@ def test_report_replay_matches_reference_format(yaml_net, tmp_path, name, tt, n_
     got = rr.report_lines(r.stderr)
     want = rr.render(keys, st, sims, params, iterations=iters, warm_up=warm, num_sims=n_sims, test_type=tt)
     assert got == want
+
+
+@pytest.mark.parametrize("name,tt,n_sims,step,ranks,extra", REPLAY_CASES[:3], ids=[c[0] for c in REPLAY_CASES[:3]])
+def test_influx_file_matches_reference_series(yaml_net, tmp_path, name, tt, n_sims, step, ranks, extra):
+    """--influx-file writes influx_db.rs's data points (series, tags, fields, Rust float
+    formatting, enqueue order of gossip_main.rs:372-645) as line protocol; with a time
+    base the timestamps are reproducible and checked too."""
+    path, keys, st, pks = yaml_net
+    iters, warm, seed, base = 24, 4, 77, 1_700_000_000_000_000_000
+    params = sweep_params(tt, n_sims, iterations=iters, warm_up=warm, step=step, ranks=ranks,
+                          fraction=0.1, when=3 if tt == 5 else 0)
+    sims = oracle_sims(pks, st, params, seed=seed)
+    res, lp = str(tmp_path / "r.txt"), str(tmp_path / "influx.lp")
+    rr.write_results(res, sims)
+    args = ["--accounts-from-yaml", "--account-file", path, "--iterations", iters, "--warm-up-rounds", warm,
+            "--replay-results", res, "--seed", seed, "--influx-file", lp, "--influx-time-base", base]
+    if tt:
+        args += ["--test-type", name, "--num-simulations", n_sims, "--step-size", step]
+    cli(*args, *extra)
+    got = open(lp).read().splitlines()
+    want = ir.render(len(st), sims, params, iterations=iters, warm_up=warm, num_sims=n_sims, test_type=tt,
+                     step=step, api=path, base=base)
+    assert got == want
+    assert got[0].startswith("simulation_config,") and got[-1].startswith("iteration,")
+
+
+def test_influx_http_refused(yaml_net):
+    r = cli("--accounts-from-yaml", "--account-file", yaml_net[0], "--influx", "l", check=False)
+    assert r.returncode == 1 and "not available offline" in r.stderr
 
 
 def test_report_empty_collection_warns(yaml_net, tmp_path):
