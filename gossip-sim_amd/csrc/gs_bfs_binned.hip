@@ -628,6 +628,7 @@ hipError_t launch_bfs_binned(Engine& e, bool record) {
   a.N = e.N; a.ASZ = e.ASZ; a.fanout = e.fanout; a.fc = e.fcap; a.capin = e.capin; a.Gmax = e.bin.Gmax;
   a.PW = e.bin.PW; a.BS = e.bin.BS; a.nbins = e.bin.nbins; a.ORW = e.ASZP + 4; a.csr_cap = e.bin.csr_cap;
   a.qmin = (e.prm.flags & GS_FLAG_BINNED_ALL_LEVELS) ? 1u : BIN_MIN_FRONTIER;
+  if (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) a.csr_cap = 256;  // small tests reach the gather's direct placement
   a.PAIRS = e.PAIRS; a.pool_cap = e.PAIRS * e.fcap; a.record = record ? 1 : 0;
   hipError_t r;
   if ((r = hipMemsetAsync(e.hops, 0xFF, e.PAIRS, e.st)) != hipSuccess) return r;

@@ -70,7 +70,8 @@ typedef struct gs_params {
                                    > 24 (not > 64) to its ordered single-lane consume, and the
                                    step-kernel round uses register paths for in-degree / entries
                                    <= 4 (not 16) and the wave consume for in-degree <= 8 (not 64)
-                                   (same results; lets small test clusters cover every path);
+                                   and the binned gather places records directly beyond 256
+                                   per bin (same results; lets small test clusters cover every path);
                                    GS_FLAG_BINNED_ALL_LEVELS: GS_BFS_BINNED bins every level, not
                                    only levels with >= 2^17 frontier pairs (same results);
                                    GS_FLAG_WIDE_RECORDS: GS_BFS_BINNED keeps 8-byte push records

@@ -250,7 +250,7 @@ def test_rotation_round_sequence_and_deferred_clear():
 
 
 @pytest.mark.parametrize("mode,narrow", [(gs.GS_BFS_LEVEL, False), (gs.GS_BFS_BINNED, False),
-                                         (gs.GS_BFS_LEVEL, True)])
+                                         (gs.GS_BFS_LEVEL, True), (gs.GS_BFS_BINNED, True)])
 def test_fused_round_matches_steps(mode, narrow):
     """gs_round's step-kernel path (consume + prune + apply of gs_consume_g.hip: register,
     wave and serial consume paths, register and wave prune paths) == the step-by-step
