@@ -57,10 +57,10 @@ struct BinArgs {
   uint32_t* T;     // [Gmax][nbins + 1] bin starts of each expand workgroup's run (+ its total)
   void* pool;      // apply -> gather: per (level, bin) runs (RecW / RecN)
   uint2* Lt;       // [256][nbins] (pool start, count) of bin b's run at level d
-  uint32_t* pool_top;
+  uint32_t* binoff;  // [nbins] records in bin b's pool region so far this round (only bin b's apply touches it)
   uint32_t* visbm;  // [PAIRS / 32] visited pairs (hop != unreached) of this round
   uint32_t N, ASZ, fanout, fc, capin, Gmax, PW, BS, nbins, ORW, csr_cap, qmin;
-  size_t PAIRS, pool_cap;
+  size_t PAIRS, pool_bin_cap;  // pool region of a bin: 2^BS * capin records (in-degrees are <= capin)
   int record;
 };
 
@@ -317,12 +317,14 @@ __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t
     return;
   }
   // 2. the level's pool run for this bin
-  if (tid == 0) {
-    const uint32_t base = atomicAdd(a.pool_top, total);
-    ctl[0] = base;
+  if (tid == 0) {  // the bin's own pool region: no device-wide counter
+    const uint32_t used = a.binoff[b];
+    const size_t base = (size_t)b * a.pool_bin_cap + used;
+    ctl[0] = (uint32_t)base;
     ctl[2] = 0;
-    if ((size_t)base + total > a.pool_cap) { atomicOr(a.err, ERR_INBOUND); ctl[2] = 1; }
-    Ltd[b] = make_uint2(base, ctl[2] ? 0u : total);
+    if ((size_t)used + total > a.pool_bin_cap) { atomicOr(a.err, ERR_INBOUND); ctl[2] = 1; }
+    else a.binoff[b] = used + total;
+    Ltd[b] = make_uint2((uint32_t)base, ctl[2] ? 0u : total);
   }
   __syncthreads();
   const uint32_t pbase = ctl[0];
@@ -525,7 +527,7 @@ __global__ void k_bin_seed(BinArgs a, const uint32_t* __restrict__ origin, uint3
   a.hops[p] = 0;
   atomicOr(&a.visbm[p >> 5], 1u << (p & 31));
   q0[o] = (uint32_t)p;
-  if (o == 0) { a.lvl[0] = S; *a.pool_top = 0; }
+  if (o == 0) a.lvl[0] = S;
 }
 
 }  // namespace gs
@@ -623,17 +625,18 @@ hipError_t launch_bfs_binned(Engine& e, bool record) {
   a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.own = e.own; a.frank = e.frank; a.origin = e.origin;
   a.obkt = e.obkt; a.nfail = e.nfail; a.mask = e.mask; a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb;
   a.egress = e.egress; a.egress_acc = e.egress_acc; a.lvl = e.lvl; a.err = e.err; a.area = e.bin_area;
-  a.T = e.bin_T; a.pool = e.bin_pool; a.Lt = e.bin_Lt; a.pool_top = e.bin_pool_top;
+  a.T = e.bin_T; a.pool = e.bin_pool; a.Lt = e.bin_Lt; a.binoff = e.bin_binoff;
   a.visbm = e.bin_vis;
   a.N = e.N; a.ASZ = e.ASZ; a.fanout = e.fanout; a.fc = e.fcap; a.capin = e.capin; a.Gmax = e.bin.Gmax;
   a.PW = e.bin.PW; a.BS = e.bin.BS; a.nbins = e.bin.nbins; a.ORW = e.ASZP + 4; a.csr_cap = e.bin.csr_cap;
   a.qmin = (e.prm.flags & GS_FLAG_BINNED_ALL_LEVELS) ? 1u : BIN_MIN_FRONTIER;
   if (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) a.csr_cap = 256;  // small tests reach the gather's direct placement
-  a.PAIRS = e.PAIRS; a.pool_cap = e.PAIRS * e.fcap; a.record = record ? 1 : 0;
+  a.PAIRS = e.PAIRS; a.pool_bin_cap = ((size_t)1 << e.bin.BS) * e.capin; a.record = record ? 1 : 0;
   hipError_t r;
   if ((r = hipMemsetAsync(e.hops, 0xFF, e.PAIRS, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.cnt, 0, e.PAIRS * 4, e.st)) != hipSuccess) return r;
+  if ((r = hipMemsetAsync(e.bin_binoff, 0, (size_t)e.bin.nbins * 4, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.bin_vis, 0, (e.PAIRS + 31) / 32 * 4, e.st)) != hipSuccess) return r;
   hipLaunchKernelGGL(k_bin_seed, dim3((e.S + 255) / 256), dim3(256), 0, e.st, a, e.origin, e.S, e.q[0]);
   return e.bin.narrow ? run_binned<RecN>(e, a) : run_binned<RecW>(e, a);

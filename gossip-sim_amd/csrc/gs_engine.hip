@@ -232,9 +232,10 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
     ALLOC(e->own, N * (e->ASZP + 4), 0);
     ALLOC(e->bin_area, PAIRS * e->fcap, 0);
     ALLOC(e->bin_T, e->bin.T_words, 0);
-    ALLOC(e->bin_pool, PAIRS * e->fcap, 0);
+    // pool: one region of 2^BS * capin records per bin (u32 records when narrow)
+    ALLOC(e->bin_pool, ((size_t)e->bin.nbins << e->bin.BS) * e->capin / (e->bin.narrow ? 2 : 1), 0);
     ALLOC(e->bin_Lt, (size_t)256 * e->bin.nbins, 0);
-    ALLOC(e->bin_pool_top, 1, 0);
+    ALLOC(e->bin_binoff, e->bin.nbins, 0);
     ALLOC(e->bin_vis, (PAIRS + 31) / 32, 0);
   }
   ALLOC(e->lvl, 256, 0);

@@ -82,9 +82,9 @@ struct Engine {
   uint32_t* own = nullptr;      // [N][ASZP + 4] own-bucket entry rows (word ASZP = hl | bucket << 16)
   uint2* bin_area = nullptr;    // expand -> apply records (pair, src), per level, PAIRS * fcap
   uint32_t* bin_T = nullptr;    // [Gmax][nbins + 1] bin starts of each expand workgroup's run
-  uint2* bin_pool = nullptr;    // apply -> gather records (local pair, hop << 24 | src), PAIRS * fcap
+  uint2* bin_pool = nullptr;    // apply -> gather records: one region of 2^BS * capin records per bin
   uint2* bin_Lt = nullptr;      // [256][nbins] (pool start, count) per level and bin
-  uint32_t* bin_pool_top = nullptr;
+  uint32_t* bin_binoff = nullptr;  // [nbins] records used in each bin's pool region this round
   uint32_t* bin_vis = nullptr;  // [PAIRS / 32] visited bitmap of the round
   // rotation
   uint32_t* rot_list = nullptr;
