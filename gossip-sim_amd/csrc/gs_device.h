@@ -117,7 +117,7 @@ __device__ inline uint32_t prefix_search(const uint64_t* __restrict__ P, uint32_
 
 // prefix_search with a coarse table PS[j] = P[min(j * PS_STRIDE, n)] (L2-resident): the
 // coarse search narrows the answer to one stride of P (2 KiB), the fine one finishes it.
-constexpr uint32_t PS_LOG = 8, PS_STRIDE = 1u << PS_LOG;
+constexpr uint32_t PS_LOG = 5, PS_STRIDE = 1u << PS_LOG;
 __host__ __device__ inline uint32_t ps_count(uint32_t n) { return (n >> PS_LOG) + 2; }
 __device__ inline uint32_t prefix_search2(const uint64_t* __restrict__ P, const uint64_t* __restrict__ PS,
                                           uint32_t n, uint64_t x) {
