@@ -554,7 +554,24 @@ __device__ inline void wave_hop_stats(const uint32_t* hist, uint32_t* ctrl) {
   }
 }
 
-template <int ASZP, bool OFF16>
+// The peers of the pushed ring slots, compacted in slot order into dst[0, popc(pushm))
+// (the rest 0). The LDS atomics that follow then cover FP lanes' words instead of
+// every ring slot: at fanout 6 that halves the atomics of the BFS and the CSR scatter.
+template <int ASZP, int FP>
+__device__ inline void compact_push(const uint32_t (&row)[ASZP], uint32_t pushm, uint32_t (&dst)[FP]) {
+#pragma unroll
+  for (int t = 0; t < FP; ++t) dst[t] = 0;
+#pragma unroll
+  for (int s = 0; s < ASZP; ++s) {
+    const uint32_t j = (uint32_t)__popc(pushm & ((1u << s) - 1u));
+    const bool b = (pushm >> s) & 1u;
+#pragma unroll
+    for (int t = 0; t < FP; ++t)
+      if (b && j == (uint32_t)t) dst[t] = row[s];
+  }
+}
+
+template <int ASZP, bool OFF16, int FP>
 __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundArgs a) {
   using PMT = typename std::conditional<(ASZP <= 16), uint16_t, uint32_t>::type;
   using OFFT = typename std::conditional<OFF16, uint16_t, uint32_t>::type;
@@ -613,6 +630,48 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
     }
   }
   if (tid == 0) { ctrl[C_LVL] = 1; hops_l[org] = 0; q0[0] = (uint16_t)org; }
+  __syncthreads();  // the rotation clear above changes mk_l
+  // Every node's pushes for this origin depend only on its row, the slot's prune
+  // mask and the failed set, not on the traversal. They are taken here for all
+  // nodes at once (two rows in flight per thread) and kept as u16 lists in the
+  // record area (stride fcap; the CSR overwrites it after the BFS), so the BFS levels
+  // issue no global loads.
+  uint16_t* lst_l = reinterpret_cast<uint16_t*>(smem + L.rec);
+  const uint32_t fc = a.fcap;
+  for (uint32_t v0 = tid; v0 < N; v0 += 2 * RWG_THREADS) {
+    const uint32_t v1 = v0 + RWG_THREADS;
+    const bool h1 = v1 < N;
+    uint32_t r0[ASZP], r1[ASZP];
+    const uint32_t nl0 = nl_l[v0], nl1 = h1 ? nl_l[v1] : 0u;
+    load_row<ASZP>(a.peers + (size_t)(v0 * NB + (nl0 >> 11)) * ASZP, r0);
+    if (h1) load_row<ASZP>(a.peers + (size_t)(v1 * NB + (nl1 >> 11)) * ASZP, r1);
+    uint32_t pm0 = taken_slots<ASZP>(r0, nl0 & 31u, (nl0 >> 5) & 63u, a.ASZ, mk_l[v0], org, a.fanout);
+    uint32_t pm1 = 0;
+    if (h1) pm1 = taken_slots<ASZP>(r1, nl1 & 31u, (nl1 >> 5) & 63u, a.ASZ, mk_l[v1], org, a.fanout);
+    if (nf) {  // failed peers burn their fanout slot (gossip.rs:538-541)
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        if (((pm0 >> s) & 1u) && a.frank[r0[s]] < nf) pm0 &= ~(1u << s);
+        if (((pm1 >> s) & 1u) && a.frank[r1[s]] < nf) pm1 &= ~(1u << s);
+      }
+    }
+    pm_l[v0] = (PMT)pm0;
+    uint32_t d0[FP];
+    compact_push<ASZP, FP>(r0, pm0, d0);
+    const uint32_t k0 = __popc(pm0);
+#pragma unroll
+    for (int j = 0; j < FP; ++j)
+      if ((uint32_t)j < k0) lst_l[v0 * fc + j] = (uint16_t)d0[j];
+    if (h1) {
+      pm_l[v1] = (PMT)pm1;
+      uint32_t d1[FP];
+      compact_push<ASZP, FP>(r1, pm1, d1);
+      const uint32_t k1 = __popc(pm1);
+#pragma unroll
+      for (int j = 0; j < FP; ++j)
+        if ((uint32_t)j < k1) lst_l[v1 * fc + j] = (uint16_t)d1[j];
+    }
+  }
   __syncthreads();
   RWG_MARK(0);
 
@@ -634,52 +693,52 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
     for (uint32_t i0 = 0; i0 < qn; i0 += RWG_THREADS) {
       if (i0 + (wid << 6) >= qn) continue;  // wave-uniform: no frontier node for this wave
       const bool valid = i0 + tid < qn;
-      uint32_t row[ASZP];
       uint32_t pushm = 0;
+      uint32_t dst[FP];
+#pragma unroll
+      for (int j = 0; j < FP; ++j) dst[j] = 0;
       if (valid) {
         const uint32_t u = cur[i0 + tid];
-        const uint32_t pmask = mk_l[u];
-        const uint32_t nl = nl_l[u];
-        load_row<ASZP>(a.peers + (size_t)(u * NB + (nl >> 11)) * ASZP, row);
-        pushm = taken_slots<ASZP>(row, nl & 31u, (nl >> 5) & 63u, a.ASZ, pmask, org, a.fanout);
-        if (nf) {  // failed peers burn their fanout slot (gossip.rs:538-541)
+        pushm = pm_l[u];
+        const uint32_t kk = __popc(pushm);
 #pragma unroll
-          for (int s = 0; s < ASZP; ++s)
-            if (((pushm >> s) & 1u) && a.frank[row[s]] < nf) pushm &= ~(1u << s);
-        }
-        pm_l[u] = (PMT)pushm;
+        for (int j = 0; j < FP; ++j)
+          if ((uint32_t)j < kk) dst[j] = lst_l[u * fc + j];
         if (a.phase_clk && tid == 0 && i0 == 0) {
           const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-          prof[0] += t1 - tl0;  // level start -> row loaded (shader cycles)
+          prof[0] += t1 - tl0;  // level start -> push list read (shader cycles)
           tl0 = t1;
         }
-      } else {
-#pragma unroll
-        for (int s = 0; s < ASZP; ++s) row[s] = 0;
       }
-      // All ring slots issue their LDS atomic back to back (slots not pushed add 0
-      // to a per-lane dummy word), then one wait: a conditional atomic per slot
-      // would be followed by its own lgkmcnt(0) wait.
-      uint32_t old[ASZP];
+      // The pushed peers (at most FP per lane) issue their LDS atomic back to back,
+      // lanes with fewer add 0 to a per-lane dummy word, then one wait: a conditional
+      // atomic per push would be followed by its own lgkmcnt(0) wait.
+      const uint32_t k = __popc(pushm);
+      uint32_t old[FP];
       uint32_t* dummy = scr + lane;
 #pragma unroll
-      for (int s = 0; s < ASZP; ++s) {
-        const bool pu = (pushm >> s) & 1u;
-        const uint32_t w = row[s], sh = (w & 1u) << 4;
-        old[s] = (atomicAdd(pu ? &cntw[w >> 1] : dummy, pu ? 1u << sh : 0u) >> sh) & 0xFFFFu;
+      for (int j = 0; j < FP; ++j) {
+        const bool pu = (uint32_t)j < k;
+        const uint32_t w = dst[j], sh = (w & 1u) << 4;
+        old[j] = (atomicAdd(pu ? &cntw[w >> 1] : dummy, pu ? 1u << sh : 0u) >> sh) & 0xFFFFu;
       }
       uint32_t newm = 0;
 #pragma unroll
-      for (int s = 0; s < ASZP; ++s)
-        if (((pushm >> s) & 1u) && old[s] == 0) {
-          newm |= 1u << s;
-          hops_l[row[s]] = (uint8_t)(d + 1);
+      for (int j = 0; j < FP; ++j)
+        if ((uint32_t)j < k && old[j] == 0) {
+          newm |= 1u << j;
+          hops_l[dst[j]] = (uint8_t)(d + 1);
         }
-      const uint32_t k = __popc(newm);
-      uint32_t idx = k ? atomicAdd(&ctrl[C_LVL + l3n], k) : 0;
+      // next-level slots: one LDS atomic per wave (a scan of the lanes' first visits)
+      const uint32_t nk = __popc(newm);
+      const uint32_t nincl = wave_incl_scan(nk);
+      const uint32_t ntot = (uint32_t)__shfl((int)nincl, 63);
+      uint32_t nb = 0;
+      if (lane == 63 && ntot) nb = atomicAdd(&ctrl[C_LVL + l3n], ntot);
+      uint32_t idx = (uint32_t)__shfl((int)nb, 63) + nincl - nk;
 #pragma unroll
-      for (int s = 0; s < ASZP; ++s)
-        if ((newm >> s) & 1u) nxt[idx++] = (uint16_t)row[s];
+      for (int j = 0; j < FP; ++j)
+        if ((newm >> j) & 1u) nxt[idx++] = (uint16_t)dst[j];
       if (a.phase_clk && tid == 0 && i0 == 0) {
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         prof[1] += t1 - tl0;  // row loaded -> pushes done
@@ -731,31 +790,27 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
       const uint32_t pm0 = hops_l[v0] != 0xFF ? pm_l[v0] : 0u;
       const uint32_t pm1 = v1 < N && hops_l[v1] != 0xFF ? pm_l[v1] : 0u;
       uint32_t r0[ASZP], r1[ASZP];
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) r0[s] = r1[s] = 0;
       if (pm0) load_row<ASZP>(a.peers + (size_t)(v0 * NB + (nl_l[v0] >> 11)) * ASZP, r0);
       if (pm1) load_row<ASZP>(a.peers + (size_t)(v1 * NB + (nl_l[v1] >> 11)) * ASZP, r1);
       eg_l[v0] = (uint8_t)__popc(pm0);
       if (v1 < N) eg_l[v1] = (uint8_t)__popc(pm1);
-      if (pm0) {
-        uint32_t pos[ASZP];
+      if (pm0 | pm1) {
+        uint32_t d0[FP], d1[FP], p0[FP], p1[FP];
+        compact_push<ASZP, FP>(r0, pm0, d0);
+        compact_push<ASZP, FP>(r1, pm1, d1);
+        const uint32_t k0 = __popc(pm0), k1 = __popc(pm1);
 #pragma unroll
-        for (int s = 0; s < ASZP; ++s) {
-          const bool pu = (pm0 >> s) & 1u;
-          pos[s] = off_fetch_inc<OFF16>(offw, r0[s], pu, dummy);
-        }
+        for (int j = 0; j < FP; ++j) p0[j] = off_fetch_inc<OFF16>(offw, d0[j], (uint32_t)j < k0, dummy);
 #pragma unroll
-        for (int s = 0; s < ASZP; ++s)
-          if ((pm0 >> s) & 1u) rec_l[pos[s]] = (uint16_t)v0;
-      }
-      if (pm1) {
-        uint32_t pos[ASZP];
+        for (int j = 0; j < FP; ++j) p1[j] = off_fetch_inc<OFF16>(offw, d1[j], (uint32_t)j < k1, dummy);
 #pragma unroll
-        for (int s = 0; s < ASZP; ++s) {
-          const bool pu = (pm1 >> s) & 1u;
-          pos[s] = off_fetch_inc<OFF16>(offw, r1[s], pu, dummy);
-        }
+        for (int j = 0; j < FP; ++j)
+          if ((uint32_t)j < k0) rec_l[p0[j]] = (uint16_t)v0;
 #pragma unroll
-        for (int s = 0; s < ASZP; ++s)
-          if ((pm1 >> s) & 1u) rec_l[pos[s]] = (uint16_t)v1;
+        for (int j = 0; j < FP; ++j)
+          if ((uint32_t)j < k1) rec_l[p1[j]] = (uint16_t)v1;
       }
     }
   }
@@ -911,16 +966,24 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   RWG_MARK(5);
 }
 
-template <int ASZP, bool OFF16>
-static hipError_t launch_rwg(Engine& e, const RoundArgs& a, size_t lds) {
+template <int ASZP, bool OFF16, int FP>
+static hipError_t launch_rwg_fp(Engine& e, const RoundArgs& a, size_t lds) {
   if (e.rwg_attr_lds != lds) {
-    hipError_t r = hipFuncSetAttribute((const void*)k_round_wg<ASZP, OFF16>,
+    hipError_t r = hipFuncSetAttribute((const void*)k_round_wg<ASZP, OFF16, FP>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (r != hipSuccess) return r;
     e.rwg_attr_lds = lds;
   }
-  hipLaunchKernelGGL((k_round_wg<ASZP, OFF16>), dim3(e.S), dim3(RWG_THREADS), lds, e.st, a);
+  hipLaunchKernelGGL((k_round_wg<ASZP, OFF16, FP>), dim3(e.S), dim3(RWG_THREADS), lds, e.st, a);
   return hipSuccess;
+}
+
+template <int ASZP, bool OFF16>
+static hipError_t launch_rwg(Engine& e, const RoundArgs& a, size_t lds) {
+  // FP: compacted pushes per lane (fanout <= 6, the reference's default, or the ring)
+  constexpr int FP6 = ASZP < 6 ? ASZP : 6;
+  if (a.fcap <= (uint32_t)FP6) return launch_rwg_fp<ASZP, OFF16, FP6>(e, a, lds);
+  return launch_rwg_fp<ASZP, OFF16, ASZP>(e, a, lds);
 }
 
 hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_slot, bool rot_clear) {
