@@ -783,7 +783,40 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   // end of the kernel (F), since VMEM operations complete in order and a load issued
   // behind them waits for them. Two nodes per thread per step, both rows in flight.
   uint8_t* eg_l = smem + L.eg;
-  {
+  constexpr uint32_t CSR_NPT = 4;  // nodes per thread of the register-staged CSR
+  if (FP <= 8 && N <= CSR_NPT * RWG_THREADS) {
+    // The push lists (in the record area) are read into registers, two u16 ids per
+    // word, then after a barrier the records overwrite them: no row is read again.
+    constexpr int FW = (FP + 1) / 2;
+    uint32_t pk[CSR_NPT][FW], kk[CSR_NPT];
+#pragma unroll
+    for (uint32_t i = 0; i < CSR_NPT; ++i) {
+      const uint32_t v = tid + i * RWG_THREADS;
+      const uint32_t pm = v < N && hops_l[v] != 0xFF ? pm_l[v] : 0u;
+      kk[i] = __popc(pm);
+      if (v < N) eg_l[v] = (uint8_t)kk[i];
+#pragma unroll
+      for (int w = 0; w < FW; ++w) {
+        const uint32_t lo = (uint32_t)(2 * w) < kk[i] ? lst_l[v * fc + 2 * w] : 0u;
+        const uint32_t hi = (uint32_t)(2 * w + 1) < kk[i] ? lst_l[v * fc + 2 * w + 1] : 0u;
+        pk[i][w] = lo | hi << 16;
+      }
+    }
+    __syncthreads();
+    uint32_t* dummy = scr + lane;
+#pragma unroll
+    for (uint32_t i = 0; i < CSR_NPT; ++i) {
+      if (!kk[i]) continue;
+      const uint32_t v = tid + i * RWG_THREADS;
+      uint32_t pos[FP];
+#pragma unroll
+      for (int j = 0; j < FP; ++j)
+        pos[j] = off_fetch_inc<OFF16>(offw, (pk[i][j >> 1] >> ((j & 1) * 16)) & 0xFFFFu, (uint32_t)j < kk[i], dummy);
+#pragma unroll
+      for (int j = 0; j < FP; ++j)
+        if ((uint32_t)j < kk[i]) rec_l[pos[j]] = (uint16_t)v;
+    }
+  } else {
     uint32_t* dummy = scr + lane;
     for (uint32_t v0 = tid; v0 < N; v0 += 2 * RWG_THREADS) {
       const uint32_t v1 = v0 + RWG_THREADS;
