@@ -656,20 +656,13 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
       }
     }
     pm_l[v0] = (PMT)pm0;
-    uint32_t d0[FP];
-    compact_push<ASZP, FP>(r0, pm0, d0);
-    const uint32_t k0 = __popc(pm0);
+    if (h1) pm_l[v1] = (PMT)pm1;
+    // pushed slots in FIFO-free slot order, each a predicated u16 store at a running index
+    uint32_t j0 = v0 * fc, j1 = v1 * fc;
 #pragma unroll
-    for (int j = 0; j < FP; ++j)
-      if ((uint32_t)j < k0) lst_l[v0 * fc + j] = (uint16_t)d0[j];
-    if (h1) {
-      pm_l[v1] = (PMT)pm1;
-      uint32_t d1[FP];
-      compact_push<ASZP, FP>(r1, pm1, d1);
-      const uint32_t k1 = __popc(pm1);
-#pragma unroll
-      for (int j = 0; j < FP; ++j)
-        if ((uint32_t)j < k1) lst_l[v1 * fc + j] = (uint16_t)d1[j];
+    for (int s = 0; s < ASZP; ++s) {
+      if ((pm0 >> s) & 1u) lst_l[j0++] = (uint16_t)r0[s];
+      if ((pm1 >> s) & 1u) lst_l[j1++] = (uint16_t)r1[s];
     }
   }
   __syncthreads();
