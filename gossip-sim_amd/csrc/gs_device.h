@@ -179,6 +179,26 @@ __device__ inline void load_row(const uint32_t* __restrict__ src, uint32_t (&row
 template <int ASZP>
 __device__ inline uint32_t taken_slots(const uint32_t (&row)[ASZP], uint32_t head, uint32_t len, uint32_t S,
                                        uint32_t pmask, uint32_t origin, uint32_t fanout) {
+  if constexpr (ASZP < 32) {  // S < 32: every ring mask fits a u32, with few VALU ops
+    const uint32_t full = (1u << S) - 1u;
+    const uint32_t lm = len >= S ? full : (1u << len) - 1u;            // ring positions [0, len)
+    const uint32_t valid = ((lm << head) | (lm >> (S - head))) & full;  // their physical slots
+    uint32_t om = 0;
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) om |= (uint32_t)(row[s] == origin) << s;
+    const uint32_t elig = valid & ~pmask & ~om;
+    uint32_t fifo = ((elig >> head) | (elig << (S - head))) & full;  // bit = ring position (FIFO order)
+    if ((uint32_t)__popc(fifo) > fanout) {
+      uint32_t sel = 0;
+      for (uint32_t t = 0; t < fanout; ++t) {
+        const uint32_t low = fifo & (~fifo + 1u);
+        sel |= low;
+        fifo ^= low;
+      }
+      fifo = sel;
+    }
+    return ((fifo << head) | (fifo >> (S - head))) & full;
+  }
   uint32_t elig = 0;
 #pragma unroll
   for (int s = 0; s < ASZP; ++s) {
