@@ -722,13 +722,18 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
           newm |= 1u << j;
           hops_l[dst[j]] = (uint8_t)(d + 1);
         }
-      // next-level slots: one LDS atomic per wave (a scan of the lanes' first visits)
-      const uint32_t nk = __popc(newm);
-      const uint32_t nincl = wave_incl_scan(nk);
-      const uint32_t ntot = (uint32_t)__shfl((int)nincl, 63);
+      // next-level slots: one LDS atomic per wave; the lanes' offsets come from one
+      // ballot per push column (mbcnt of the lower lanes), no LDS round trips
+      uint32_t nex = 0, ntot = 0;
+#pragma unroll
+      for (int j = 0; j < FP; ++j) {
+        const uint64_t bj = __ballot((newm >> j) & 1u);
+        nex += __builtin_amdgcn_mbcnt_hi((uint32_t)(bj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bj, 0u));
+        ntot += (uint32_t)__popcll(bj);
+      }
       uint32_t nb = 0;
-      if (lane == 63 && ntot) nb = atomicAdd(&ctrl[C_LVL + l3n], ntot);
-      uint32_t idx = (uint32_t)__shfl((int)nb, 63) + nincl - nk;
+      if (lane == 0 && ntot) nb = atomicAdd(&ctrl[C_LVL + l3n], ntot);
+      uint32_t idx = __builtin_amdgcn_readfirstlane(nb) + nex;
 #pragma unroll
       for (int j = 0; j < FP; ++j)
         if ((newm >> j) & 1u) nxt[idx++] = (uint16_t)dst[j];
