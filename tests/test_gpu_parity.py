@@ -456,6 +456,37 @@ def test_fused_round_heavy_paths():
     assert max_in > 24
 
 
+def fused_vs_split(n, S, rounds, *, checks, **kw):
+    pks, st = eb.synth.network(n)
+    engines = [gs.Engine(st, S, seed=5, bfs_mode=gs.GS_BFS_WORKGROUP, split_round=f, **kw) for f in (False, True)]
+    assert engines[0].info()["fused_round"] and not engines[1].info()["fused_round"]
+    for e in engines:
+        e.set_slots([(k * 5) % n for k in range(S)], 2, 0.15)
+        e.init_active_sets()
+    for r in range(rounds):
+        for e in engines:
+            e.round(r, record=r >= 5)
+    a, b = engines
+    np.testing.assert_array_equal(a.summaries(), b.summaries())
+    for k in checks:
+        np.testing.assert_array_equal(a.hops(k), b.hops(k))
+        np.testing.assert_array_equal(a.pruned_all(k), b.pruned_all(k))
+        for x, y in zip(a.caches(k), b.caches(k)):
+            np.testing.assert_array_equal(x, y)
+        for x, y in zip(a.accumulators(k), b.accumulators(k)):
+            np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("n,fanout,asz", [
+    (3500, 6, 12),  # > 3,072 nodes: the CSR reloads rows instead of staging the push lists
+    (600, 8, 8),    # 8 pushes per lane: register-staged CSR at its widest
+    (500, 7, 16),   # fanout > 6: push columns = ring slots, CSR from rows
+])
+def test_fused_round_matches_split_round_shapes(n, fanout, asz):
+    """The one-kernel round's push-list / CSR variants == the split kernels, through a prune wave."""
+    fused_vs_split(n, 24, 45, checks=(0, 11, 23), fanout=fanout, active_set_size=asz, rotation_probability=0.03)
+
+
 def test_fused_round_matches_split_round():
     """One-kernel round == split kernels (WG BFS + consume/prune + stats) incl. summaries."""
     pks, st = eb.synth.network(400)
