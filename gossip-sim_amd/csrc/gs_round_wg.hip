@@ -781,7 +781,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   // end of the kernel (F), since VMEM operations complete in order and a load issued
   // behind them waits for them. Two nodes per thread per step, both rows in flight.
   uint8_t* eg_l = smem + L.eg;
-  constexpr uint32_t CSR_NPT = 4;  // nodes per thread of the register-staged CSR
+  constexpr uint32_t CSR_NPT = (3072 + RWG_THREADS - 1) / RWG_THREADS;  // nodes per thread of the register-staged CSR
   if (FP <= 8 && N <= CSR_NPT * RWG_THREADS) {
     // The push lists (in the record area) are read into registers, two u16 ids per
     // word, then after a barrier the records overwrite them: no row is read again.
