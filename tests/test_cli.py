@@ -122,7 +122,15 @@ def sweep_params(test_type, n_sims, *, iterations, warm_up, step, ranks=(1,), fa
         q = dict(fanout=fanout, asz=asz, iterations=iterations, origin_rank=ranks[0], p=p, thr=thr, min_ingress=mi,
                  fraction=fraction, when_to_fail=when, test_type=test_type, num_sims=n_sims, step_size=step,
                  warm_up=warm_up)
-        if test_type == 6:
+        if test_type == 1:  # gossip_main.rs:775-797
+            q["asz"] = asz + i * int(step)
+        elif test_type == 3:  # gossip_main.rs:798-825: the active set grows to the fanout
+            q["fanout"] = fanout + i * int(step)
+            if q["fanout"] > q["asz"]:
+                q["asz"] = q["fanout"]
+        elif test_type == 7:  # gossip_main.rs:915-937
+            q["p"] = p + i * float(step)
+        elif test_type == 6:
             q["origin_rank"] = ranks[i]
         elif test_type == 5:
             q["fraction"] = fraction + i * float(step)
@@ -142,7 +150,12 @@ REPLAY_CASES = [
     ("fail-nodes", 5, 2, 0.2, (1,), ["--fraction-to-fail", 0.1, "--when-to-fail", 3, "--origin-rank", 1, 1, 1]),
     ("min-ingress-nodes", 2, 2, 1, (1,), ["--origin-rank", 1, 9, 9]),
     ("prune-stake-threshold", 4, 2, 0.25, (1,), ["--origin-rank", 1, 1, 1]),
+    # the engine-changing sweeps: one engine (active-set trajectory) per value
+    ("active-set-size", 1, 3, 2, (1,), ["--origin-rank", 1, 1, 1, 1]),
+    ("push-fanout", 3, 3, 4, (1,), ["--origin-rank", 1, 1, 1, 1]),  # fanout 14 > 12 raises the set to 14
+    ("rotate-probability", 7, 3, 0.25, (1,), ["--origin-rank", 1, 1, 1, 1]),
 ]
+ENGINE_SWEEPS = REPLAY_CASES[5:]
 
 
 @pytest.mark.parametrize("name,tt,n_sims,step,ranks,extra", REPLAY_CASES, ids=[c[0] for c in REPLAY_CASES])
@@ -230,3 +243,29 @@ def test_cli_run_matches_oracle(yaml_net, tmp_path, gpus):
             np.testing.assert_array_equal(gu[n], wu[n], err_msg=f"sim {k} {n}")
     assert rr.report_lines(r.stderr) == rr.render(keys, st, want, params, iterations=iters, warm_up=warm,
                                                   num_sims=3, test_type=6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,tt,n_sims,step,ranks,extra", ENGINE_SWEEPS, ids=[c[0] for c in ENGINE_SWEEPS])
+def test_cli_engine_sweeps_match_oracle(yaml_net, tmp_path, name, tt, n_sims, step, ranks, extra):
+    """The sweeps that change the engine itself (gossip_main.rs:775-825,915-937): the
+    active-set size, the push fanout (with its raise of the active-set size to the fanout,
+    :809-811) and the rotation probability. The CLI runs one engine per value on the GPU;
+    every sim's result arrays equal the oracle's run_simulation with that value, and the
+    report equals the reference-format rendering."""
+    path, keys, st, pks = yaml_net
+    iters, warm, seed = 34, 6, 13
+    params = sweep_params(tt, n_sims, iterations=iters, warm_up=warm, step=step, ranks=ranks)
+    res = str(tmp_path / "g.txt")
+    r = cli("--accounts-from-yaml", "--account-file", path, "--iterations", iters, "--warm-up-rounds", warm,
+            "--test-type", name, "--num-simulations", n_sims, "--step-size", step, *extra,
+            "--print-stats", "--save-results", res, "--seed", seed, "--gpus", 2)
+    got = rr.read_results(res)
+    want = oracle_sims(pks, st, params, seed=seed)
+    for k, ((gf, gu), (wf, wu)) in enumerate(zip(got, want)):
+        for n in F64_NAMES:
+            np.testing.assert_array_equal(gf[n], wf[n], err_msg=f"{name} sim {k} {n}")
+        for n in U64_NAMES:
+            np.testing.assert_array_equal(gu[n], wu[n], err_msg=f"{name} sim {k} {n}")
+    assert rr.report_lines(r.stderr) == rr.render(keys, st, want, params, iterations=iters, warm_up=warm,
+                                                  num_sims=n_sims, test_type=tt)

@@ -389,14 +389,15 @@ def test_binned_bfs_matches_level_bfs_large(all_levels, wide):
 
 # ------------------------------------------- one-kernel workgroup round ----
 def run_fused_parity(n, S, rounds, *, fanout=6, asz=12, p=0.02, thr=0.15, mi=2, seed=11, check=(0, 1, 2, 3),
-                     fail_at=None, fraction=0.0, full_every=5, narrow=False):
+                     fail_at=None, fraction=0.0, full_every=5, narrow=False, origins=None, record_from=3):
     """gs_round's one-kernel workgroup round against the oracle, round by round, on
     `check` slots of an S-slot engine (the other slots run alongside)."""
     pks, st = eb.synth.network(n)
     eng = gs.Engine(st, S, fanout=fanout, active_set_size=asz, rotation_probability=p, seed=seed,
                     bfs_mode=gs.GS_BFS_WORKGROUP, narrow_wave_path=narrow)
     assert eng.info()["fused_round"]
-    origins = [(k * 37 + 1) % n for k in range(S)]
+    if origins is None:
+        origins = [(k * 37 + 1) % n for k in range(S)]
     eng.set_slots(origins, mi, thr)
     eng.init_active_sets()
     sims = {k: ob.Sim(ob.PHILOX, seed, pks, st, fanout) for k in check}
@@ -408,7 +409,7 @@ def run_fused_parity(n, S, rounds, *, fanout=6, asz=12, p=0.02, thr=0.15, mi=2, 
             eng.fail_nodes([fraction] * S)
             for s in sims.values():
                 s.fail_nodes(fraction)
-        eng.round(r, record=r >= 3)
+        eng.round(r, record=r >= record_from)
         for k, s in sims.items():
             o = origins[k]
             s.run_gossip(o)
@@ -456,12 +457,12 @@ def test_fused_round_heavy_paths():
     assert max_in > 24
 
 
-def fused_vs_split(n, S, rounds, *, checks, **kw):
+def fused_vs_split(n, S, rounds, *, checks, seed=5, origins=None, **kw):
     pks, st = eb.synth.network(n)
-    engines = [gs.Engine(st, S, seed=5, bfs_mode=gs.GS_BFS_WORKGROUP, split_round=f, **kw) for f in (False, True)]
+    engines = [gs.Engine(st, S, seed=seed, bfs_mode=gs.GS_BFS_WORKGROUP, split_round=f, **kw) for f in (False, True)]
     assert engines[0].info()["fused_round"] and not engines[1].info()["fused_round"]
     for e in engines:
-        e.set_slots([(k * 5) % n for k in range(S)], 2, 0.15)
+        e.set_slots(origins if origins is not None else [(k * 5) % n for k in range(S)], 2, 0.15)
         e.init_active_sets()
     for r in range(rounds):
         for e in engines:
@@ -507,4 +508,138 @@ def test_fused_round_matches_split_round():
         for x, y in zip(a.caches(k), b.caches(k)):
             np.testing.assert_array_equal(x, y)
         for x, y in zip(a.accumulators(k), b.accumulators(k)):
+            np.testing.assert_array_equal(x, y)
+
+
+# ------------------------------------------------------- BASELINE configs at size ----
+C2_SEED = 0x5EED0003  # bench.py's simulation seed
+
+
+def test_fused_round_parity_c2_size():
+    """BASELINE C2 at its real size, on bench.py's own engine: N = 3,000 power-law nodes,
+    all 3,000 origins batched (origin of slot s = node s), p = 0.01, seed 0x5EED0003.
+    Six slots are compared with the oracle every round through the first prune wave
+    (hops, prune sets, counters; caches and prune state every 6 rounds). Every node id
+    >= 768 is reached and pushes, so k_round_wg's register-staged CSR runs all of its
+    CSR_NPT = 4 iterations per thread (gs_round_wg.hip, nodes 768..3071)."""
+    n = 3000
+    eng, total, max_in = run_fused_parity(n, n, 28, p=0.01, seed=C2_SEED, origins=list(range(n)),
+                                          check=(0, 1, 767, 768, 2047, 2999), full_every=6, record_from=20)
+    assert total > 0  # the first prune wave (~round 20) was compared
+    assert max_in > 6
+    summ = eng.summaries()
+    assert summ.shape == (8, n) and int(summ["prunes"].sum()) > 0
+
+
+def test_fused_round_matches_split_round_c2_size():
+    """The same C2 engine, all 3,000 slots: the one-kernel round equals the split kernels
+    (workgroup BFS + step consume/prune + stats) for every slot's per-round summaries, and
+    hops / prune state / caches / accumulators of sampled slots, through a prune wave."""
+    n = 3000
+    fused_vs_split(n, n, 26, checks=(0, 768, 1500, 2999), seed=C2_SEED, origins=list(range(n)),
+                   rotation_probability=0.01)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_simulation_parity_c1(mode):
+    """BASELINE C1 as configured: ~1,000-node network, push fanout 6, active-set size 12,
+    origin rank 1, 200 warm-up + 100 measured iterations (p 0.013333, min-ingress 2,
+    threshold 0.15): gs_run_simulations == the oracle's run_simulation for every result
+    array (gossip_main.rs:292-647)."""
+    compare_sim(1000, ranks=[1], iterations=300, warm=200, seed=C2_SEED, p=0.013333, bfs_mode=mode)
+
+
+def _invariants(eng, k, n, summ_last, failed=None):
+    """Size-independent properties of one slot's last round (gossip.rs:494-615)."""
+    hops = eng.hops(k)
+    off, src, hop = eng.inbound(k, cap=32 * n)
+    e, i, _ = eng.counters(k)
+    E = int(off[-1])
+    assert int(i.sum()) == int(e.sum()) == E == int(summ_last["pushes"])
+    reached = hops != 0xFF
+    assert int(reached.sum()) == int(summ_last["visited"])
+    h = hops.astype(np.int64)
+    assert (hop.astype(np.int64)[:E] == h[src[:E]] + 1).all()  # orders hop = dist[src] + 1
+    has = np.diff(off) > 0
+    assert (hop[off[:-1][has]].astype(np.int64) == h[has]).all()  # first arrival sets the hop
+    assert (reached[has]).all() and int((reached & ~has).sum()) == 1  # only the origin is reached without a push
+    if failed is not None:
+        f = failed.astype(bool)
+        # pushes to failed peers are dropped (gossip.rs:538-541): only a failed origin is reached
+        assert int((reached & f & has).sum()) == 0
+        assert int(summ_last["stranded"]) == int((~reached & ~f).sum())
+    return hops
+
+
+def test_c4_sweep_slots_1m():
+    """BASELINE C4 at size: a 1M-node power-law network, origin rank 1, the fail-nodes sweep
+    (f = 0.1..0.5, when-to-fail 0) and the prune-stake-threshold sweep (0.05..0.40) as 13
+    slots of one engine, 22 rounds through the first prune wave. The binned BFS equals
+    the level BFS bit for bit (summaries of every slot every round; hops, counters and
+    accumulators at the end, inbound lists of two slots), and the size-independent
+    properties hold on every slot."""
+    n = 1_000_000
+    st = eb.synth.power_law_stakes(n)
+    origin = int(np.argmax(st))  # rank 1: the largest stake, lowest id on ties
+    fr = [0.1, 0.2, 0.3, 0.4, 0.5] + [0.0] * 8
+    thr = [0.15] * 5 + [0.05 * (j + 1) for j in range(8)]
+    S = len(fr)
+    engs = [gs.Engine(st, S, seed=C2_SEED, rotation_probability=0.013333, bfs_mode=m)
+            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED)]
+    for e in engs:
+        e.set_slots([origin] * S, 2, thr)
+        e.init_active_sets()
+        e.fail_nodes(fr)
+    for r in range(22):
+        for e in engs:
+            e.round(r, record=True)
+    a, b = engs
+    sa, sb = a.summaries(), b.summaries()
+    np.testing.assert_array_equal(sa, sb)
+    for k in range(S):
+        fa = a.failed(k)
+        assert int(fa.sum()) == int(fr[k] * n)  # floor(f * N) nodes fail (gossip.rs:756-771)
+        np.testing.assert_array_equal(fa, b.failed(k))
+        ha = _invariants(a, k, n, sa[-1, k], failed=fa) if k in (0, 4, 5, 12) else a.hops(k)
+        np.testing.assert_array_equal(ha, b.hops(k))
+        for x, y in zip(a.counters(k), b.counters(k)):
+            np.testing.assert_array_equal(x, y)
+        for x, y in zip(a.accumulators(k), b.accumulators(k)):
+            np.testing.assert_array_equal(x, y)
+    for k in (0, 12):
+        for x, y in zip(a.inbound(k, cap=32 * n), b.inbound(k, cap=32 * n)):
+            np.testing.assert_array_equal(x, y)
+    # the threshold slots share origin, trajectory and caches until they prune: at the
+    # first prune round a higher threshold keeps more inbound stake, so prunes do not grow
+    pr = sa["prunes"][:, 5:].astype(np.int64)
+    first = int(np.nonzero(pr.sum(axis=1))[0][0])
+    assert (np.diff(pr[first]) <= 0).all() and pr[first, 0] > pr[first, -1]
+    assert (sa["visited"][:, 5:] > 0.9 * n).all()
+    # more failures reach fewer nodes
+    assert (np.diff(sa["visited"][-1, :5].astype(np.int64)) < 0).all()
+
+
+def test_c3_widest_rows_100k():
+    """C3's widest active sets: 100k nodes at active-set size 27 (ring rows padded to 28
+    words), two slots, 4 rounds: binned == level bit for bit and the invariants hold."""
+    n = 100_000
+    st = eb.synth.power_law_stakes(n)
+    engs = [gs.Engine(st, 2, seed=C2_SEED, active_set_size=27, rotation_probability=0.013333, bfs_mode=m)
+            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED)]
+    for e in engs:
+        e.set_slots([int(np.argmax(st)), n // 3], 2, 0.15)
+        e.init_active_sets()
+        for r in range(4):
+            e.round(r, record=True)
+    a, b = engs
+    peers, lens = a.active_sets()
+    assert (lens == 27).all()
+    srt = np.sort(peers, axis=2)
+    assert (np.diff(srt.astype(np.int64), axis=2) != 0).all()
+    np.testing.assert_array_equal(peers, b.active_sets()[0])
+    sa = a.summaries()
+    np.testing.assert_array_equal(sa, b.summaries())
+    for k in range(2):
+        np.testing.assert_array_equal(_invariants(a, k, n, sa[-1, k]), b.hops(k))
+        for x, y in zip(a.inbound(k, cap=32 * n), b.inbound(k, cap=32 * n)):
             np.testing.assert_array_equal(x, y)
