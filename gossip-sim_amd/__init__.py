@@ -21,7 +21,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libgossip_hip.so")
 if os.environ.get("GS_LIB_VARIANT"):  # A/B builds of the same sources (scripts/), never a fallback
     LIB_PATH = os.path.join(PKG_DIR, "variants", os.environ["GS_LIB_VARIANT"], "libgossip_hip.so")
 
-GS_BFS_AUTO, GS_BFS_WORKGROUP, GS_BFS_LEVEL, GS_BFS_BINNED = 0, 1, 2, 3
+GS_BFS_AUTO, GS_BFS_WORKGROUP, GS_BFS_LEVEL, GS_BFS_BINNED, GS_BFS_MULTI = 0, 1, 2, 3, 4
 GS_FLAG_PROFILE = 1
 GS_FLAG_SPLIT_ROUND = 2
 GS_FLAG_NARROW_WAVE_PATH = 4

@@ -81,6 +81,8 @@ static void destroy_engine(Engine* e) {
   for (auto& kv : e->timers)
     for (auto& pr : kv.second.ev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (hipEvent_t x : e->ev_pool) hipEventDestroy(x);
+  for (hipEvent_t x : e->mv_ev)
+    if (x) hipEventDestroy(x);
   if (e->st) hipStreamDestroy(e->st);
   delete e;
 }
@@ -119,6 +121,8 @@ static int check_err(Engine* e) {
                                " pushes in one round; recreate the engine with a larger inbound_capacity");
   if (f & ERR_CACHE) return fail(GS_ERANGE, "received-cache capacity (96 keys) exceeded");
   if (f & ERR_DEPTH) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
+  if (f & ERR_MV_CAP)
+    return fail(GS_ERANGE, "multi-source BFS: record / frontier capacity exceeded (recreate with GS_BFS_LEVEL)");
   if (f & ERR_BOUNDS) return fail(GS_ERANGE, "debug bounds check failed (see GS_OOB lines on stdout)");
   return GS_OK;
 }
@@ -174,17 +178,23 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   const size_t pairs = (size_t)n * n_slots;
   bin_geometry(n, pairs, e->fcap, e->bin, !(prm->flags & GS_FLAG_WIDE_RECORDS));
   const bool bin_ok = pairs <= (1ull << 28) && bin_supported(e->bin, e->fcap);
+  mv_geometry(n, n_slots, e->ASZ, e->ASZP, e->mv);
+  const bool mv_ok = mv_supported(e->mv, e->ASZP);
   if (mode == GS_BFS_AUTO)
     mode = (n <= 8192 && n_slots >= 64) ? GS_BFS_WORKGROUP : (bin_ok ? GS_BFS_BINNED : GS_BFS_LEVEL);
   if (mode == GS_BFS_BINNED && !bin_ok) {
     destroy_engine(e);
     return fail(GS_EINVAL, "binned BFS: n_nodes * n_slots too large for its bin tables (use GS_BFS_LEVEL)");
   }
+  if (mode == GS_BFS_MULTI && !mv_ok) {
+    destroy_engine(e);
+    return fail(GS_EINVAL, "multi-source BFS: bin geometry exceeds LDS (use GS_BFS_LEVEL)");
+  }
   if (mode == GS_BFS_WORKGROUP && (n > 65535 || lds > 160 * 1024)) {
     destroy_engine(e);
     return fail(GS_EINVAL, "workgroup BFS needs the per-slot state (9 B/node) to fit in 160 KiB of LDS");
   }
-  if (mode != GS_BFS_WORKGROUP && mode != GS_BFS_LEVEL && mode != GS_BFS_BINNED) {
+  if (mode != GS_BFS_WORKGROUP && mode != GS_BFS_LEVEL && mode != GS_BFS_BINNED && mode != GS_BFS_MULTI) {
     destroy_engine(e);
     return fail(GS_EINVAL, "bfs_mode");
   }
@@ -238,6 +248,20 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
     ALLOC(e->bin_binoff, e->bin.nbins, 0);
     ALLOC(e->bin_vis, (PAIRS + 31) / 32, 0);
   }
+  if (mode == GS_BFS_MULTI) {
+    const MvGeom& g = e->mv;
+    ALLOC(e->own, N * (e->ASZP + 4), 0);
+    ALLOC(e->mv_vis, N, 0);
+    ALLOC(e->mv_q[0], g.q_cap, 0);
+    ALLOC(e->mv_q[1], g.q_cap, 0);
+    ALLOC(e->mv_tb, 260, 0);
+    ALLOC(e->mv_T, g.rows_cap * g.TW, 0);
+    ALLOC(e->mv_area, g.area_cap, 0);
+    ALLOC(e->mv_ctr, 4, 0);
+    ALLOC(e->mv_gtab, (size_t)((S + g.GW - 1) / g.GW) * GT_WORDS, 0);
+    ALLOC(e->mv_seed, S, 0);
+  }
+  e->h_nfail_any.assign(S, 0);
   ALLOC(e->lvl, 256, 0);
   ALLOC(e->rot_list, N, 0);
   ALLOC(e->rot_count, 2, 0);
@@ -339,6 +363,13 @@ int gs_set_slots(gs_engine* eh, const gs_slot* slots, uint32_t n_slots) {
   HIPC(hipMemcpyAsync(e->obkt, ob.data(), e->S, hipMemcpyHostToDevice, e->st));
   HIPC(hipMemcpyAsync(e->min_ingress, mi.data(), e->S * 4, hipMemcpyHostToDevice, e->st));
   HIPC(hipMemcpyAsync(e->thr, thr.data(), e->S * 8, hipMemcpyHostToDevice, e->st));
+  if (e->bfs_mode == GS_BFS_MULTI) {
+    std::vector<uint32_t> gtab;
+    std::vector<uint2> seeds;
+    mv_build_groups(*e, org, ob, bh, gtab, seeds);
+    HIPC(hipMemcpyAsync(e->mv_gtab, gtab.data(), gtab.size() * 4, hipMemcpyHostToDevice, e->st));
+    HIPC(hipMemcpyAsync(e->mv_seed, seeds.data(), seeds.size() * sizeof(uint2), hipMemcpyHostToDevice, e->st));
+  }
   e->slots.assign(slots, slots + n_slots);
   e->slots_set = true;
   int r = reset_pair_state(e);
@@ -425,6 +456,7 @@ int gs_fail_nodes(gs_engine* eh, const double* fraction) {
     if (f >= 1.8446744073709552e19) k = ~0ull;
     if (k > e->N) return fail(GS_ERANGE, "fail_nodes: fraction * n exceeds the cluster (reference panics)");
     nf[o] = std::max(nf[o], (uint32_t)k);
+    e->h_nfail_any[o] = nf[o] ? 1u : 0u;
   }
   HIPC(hipMemcpyAsync(e->nfail, nf.data(), e->S * 4, hipMemcpyHostToDevice, e->st));
   HIPC(hipStreamSynchronize(e->st));
@@ -541,7 +573,7 @@ int gs_round(gs_engine* eh, uint32_t round, int record) {
   if (int s = do_bfs(e, rec)) return s;
   if (int s = do_cp(e, true, true, true, rec)) return s;
   if (int s = gs_chance_to_rotate(eh, round)) return s;
-  if (rec) return do_stats(e, e->bfs_mode == GS_BFS_WORKGROUP ? 2 : 1);
+  if (rec) return do_stats(e, e->bfs_mode == GS_BFS_WORKGROUP ? 2 : e->bfs_mode == GS_BFS_MULTI ? 4 : 1);
   return GS_OK;
 }
 

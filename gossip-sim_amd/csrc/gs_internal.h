@@ -28,6 +28,15 @@ struct BinGeom {
   bool narrow = false;  // 4-byte records (bins of 2^11 pairs, N <= 2^21)
 };
 
+// Geometry of the multi-source frontier BFS (gs_bfs_multi.hip): bins of 2^BS nodes,
+// records u64 = src | node-in-bin << UB | slot mask << (UB + BS), slot groups of <= GW.
+constexpr uint32_t GT_WORDS = 96;  // per-group table words
+struct MvGeom {
+  uint32_t UB = 0, BS = 0, nbins = 0, GW = 0, XPT = 0, PW = 0, TW = 0, gcap = 0;
+  size_t q_cap = 0, area_cap = 0, rows_cap = 0;
+};
+struct MvGroup { uint32_t s0, sg, seed0, nseed; };
+
 struct Engine {
   gs_params prm{};
   uint32_t N = 0, S = 0;
@@ -86,6 +95,20 @@ struct Engine {
   uint2* bin_Lt = nullptr;      // [256][nbins] (pool start, count) per level and bin
   uint32_t* bin_binoff = nullptr;  // [nbins] records used in each bin's pool region this round
   uint32_t* bin_vis = nullptr;  // [PAIRS / 32] visited bitmap of the round
+  // multi-source frontier BFS (GS_BFS_MULTI, gs_bfs_multi.hip)
+  MvGeom mv{};
+  uint32_t* mv_vis = nullptr;     // [N] slot masks reached this round (current group)
+  uint2* mv_q[2] = {nullptr, nullptr};  // frontier entries (node | entry << 24, slot mask) [q_cap]
+  uint32_t* mv_tb = nullptr;      // [257] first T row of each level
+  uint32_t* mv_T = nullptr;       // [rows_cap][TW] per expand workgroup: run base, bin starts, total
+  unsigned long long* mv_area = nullptr;  // [area_cap] records of the round
+  uint32_t* mv_ctr = nullptr;     // [4] records used
+  uint32_t* mv_gtab = nullptr;    // [groups][GT_WORDS]
+  uint2* mv_seed = nullptr;       // [S] seed entries (distinct origins) of every group
+  std::vector<MvGroup> mv_groups;
+  hipEvent_t mv_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool mv_attr_set = false;
+  std::vector<uint32_t> h_nfail_any;  // host copy: slot has failed nodes
   // rotation
   uint32_t* rot_list = nullptr;
   uint32_t* rot_count = nullptr;    // [2]: rotation r counts into [r & 1] and zeroes [(r + 1) & 1]
@@ -155,6 +178,11 @@ hipError_t launch_bfs_binned(Engine& e, bool record);
 hipError_t launch_bfs_level_step(Engine& e, bool record, uint32_t d, uint32_t qmin, uint32_t qmax);
 void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g, bool allow_narrow);
 bool bin_supported(const BinGeom& g, uint32_t fcap);
+void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g);
+bool mv_supported(const MvGeom& g, uint32_t ASZP);
+void mv_build_groups(Engine& e, const std::vector<uint32_t>& origins, const std::vector<uint8_t>& obkt,
+                     const std::vector<uint8_t>& bucket, std::vector<uint32_t>& gtab, std::vector<uint2>& seeds);
+hipError_t launch_bfs_multi(Engine& e, bool record);
 // own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);

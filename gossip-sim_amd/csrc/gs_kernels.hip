@@ -553,6 +553,7 @@ hipError_t launch_bfs(Engine& e, bool record) {
     return hipGetLastError();
   }
   if (e.bfs_mode == GS_BFS_BINNED) return launch_bfs_binned(e, record);
+  if (e.bfs_mode == GS_BFS_MULTI) return launch_bfs_multi(e, record);
   if ((r = hipMemsetAsync(e.hops, 0xFF, e.PAIRS, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.cnt, 0, e.PAIRS * 4, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st)) != hipSuccess) return r;
@@ -915,8 +916,9 @@ struct StatsArgs {
 };
 
 // FULL: the step-wise gs_record_round (reads the per-round counters of every pair);
-// LITE: after a fused round whose kernels already accumulated egress/ingress/prunes.
-template <bool FULL>
+// LITE: after a fused round whose kernels already accumulated egress/ingress/prunes
+// (EG: the BFS left egress to this pass: the multi-source BFS).
+template <bool FULL, bool EG = false>
 __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
   const uint32_t o = blockIdx.y;
   const size_t base = (size_t)o * a.N;
@@ -942,7 +944,7 @@ __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
     if (hh != 0xFF) {
       ++vis;
       atomicAdd(&h[hh], 1u);
-      if (FULL) a.egress_acc[p] += a.egress[p];
+      if (FULL || EG) a.egress_acc[p] += a.egress[p];
     } else if (!(nf && a.frank[v] < nf)) {
       a.strand[p] += 1;
       ++sc;
@@ -1053,7 +1055,8 @@ __global__ __launch_bounds__(1024) void k_stats_finalize(StatsArgs a, uint32_t r
 }
 
 // mode 0: full pass; 1: hop-only pass (fused level-synchronous round); 2: finalize only
-// (the workgroup BFS already reduced the round).
+// (the workgroup BFS already reduced the round); 3: the full pass only (partition
+// partials); 4: hop pass that also accumulates egress (multi-source BFS round).
 hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   StatsArgs a;
   a.stake = e.stake; a.frank = e.frank; a.srank = e.srank; a.by_srank = e.by_srank; a.nfail = e.nfail;
@@ -1066,6 +1069,7 @@ hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   uint32_t gx = grid_for(e.N, 256, std::max<uint32_t>(64, 2048 / std::max<uint32_t>(e.S, 1)));
   if (mode == 0 || mode == 3) hipLaunchKernelGGL(k_stats_pass<true>, dim3(gx, e.S), dim3(256), 0, e.st, a);
   else if (mode == 1) hipLaunchKernelGGL(k_stats_pass<false>, dim3(gx, e.S), dim3(256), 0, e.st, a);
+  else if (mode == 4) hipLaunchKernelGGL((k_stats_pass<false, true>), dim3(gx, e.S), dim3(256), 0, e.st, a);
   if (mode != 3)  // mode 3: the pass only (a partition sums the partials over ranks first)
     hipLaunchKernelGGL(k_stats_finalize, dim3(e.S), dim3(1024), 0, e.st, a, rec_slot);
   return hipGetLastError();

@@ -3,7 +3,9 @@
 // are addressed by their index in the pubkey array the caller passed in.
 #include "oracle_sim.h"
 #include <algorithm>
+#include <chrono>
 #include <stdexcept>
+#include <thread>
 #include <string>
 
 using namespace orc;
@@ -471,6 +473,49 @@ size_t or_res_u64(void* hp, const char* name, uint64_t* out, size_t cap) {
     return put_u({(uint64_t)st.hops_histogram.errors, (uint64_t)st.stranded.histogram.errors}, out, cap);
   if (n == "failed_count") return put_u({(uint64_t)st.failed_count}, out, cap);
   return (size_t)-1;
+}
+
+// CPU baseline on all host cores (bench.py's cpu_baseline leg; test infrastructure):
+// n_sims independent reference-structure simulations (one origin each, as
+// gossip_main.rs runs them), dealt round-robin over `threads` std::threads. Every sim
+// is initialised first (init_s, wall); then every thread runs rounds [0, rounds) of
+// its sims (gossip_main.rs:449-473) and the wall time of that parallel region is
+// run_s. Returns the pushes to non-failed peers summed over sims and rounds.
+uint64_t or_bench_parallel(uint64_t seed, const uint8_t* pks, const uint64_t* stakes, size_t n, size_t fanout,
+                           size_t asz, const uint32_t* origins, size_t n_sims, double thr, size_t min_ingress, double p,
+                           uint32_t rounds, uint32_t threads, double* init_s, double* run_s) {
+  using clk = std::chrono::steady_clock;
+  if (threads < 1) threads = 1;
+  std::vector<std::unique_ptr<Sim>> sims(n_sims);
+  auto par = [&](auto&& body) {
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < threads; ++t)
+      th.emplace_back([&, t]() {
+        for (size_t i = t; i < n_sims; i += threads) body(i);
+      });
+    for (auto& x : th) x.join();
+  };
+  const auto t0 = clk::now();
+  par([&](size_t i) {
+    sims[i].reset(new Sim(PHILOX, seed, pk_vec(pks, n), std::vector<uint64_t>(stakes, stakes + n), fanout));
+    sims[i]->init_philox(asz);
+  });
+  const auto t1 = clk::now();
+  std::vector<uint64_t> edges(n_sims, 0);
+  par([&](size_t i) {
+    Sim* s = sims[i].get();
+    const Pubkey org = s->nodes[origins[i]].pk;
+    for (uint32_t r = 0; r < rounds; ++r) {
+      s->round_steps(org, thr, min_ingress, asz, p, r, nullptr);
+      for (auto& kv : s->cluster.ingress_message_count) edges[i] += kv.second;
+    }
+  });
+  const auto t2 = clk::now();
+  *init_s = std::chrono::duration<double>(t1 - t0).count();
+  *run_s = std::chrono::duration<double>(t2 - t1).count();
+  uint64_t e = 0;
+  for (uint64_t x : edges) e += x;
+  return e;
 }
 
 }  // extern "C"

@@ -17,7 +17,7 @@ gs = eb.gs
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 U64MAX = np.uint64(2**64 - 1)
-MODES = [gs.GS_BFS_WORKGROUP, gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED]
+MODES = [gs.GS_BFS_WORKGROUP, gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI]
 
 
 def ekw(mode):
@@ -206,7 +206,7 @@ def test_round_by_round_parity(mode):
     assert total > 0  # the ~20-round prune waves were exercised
 
 
-@pytest.mark.parametrize("mode", [gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED])
+@pytest.mark.parametrize("mode", [gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI])
 def test_parity_sweep_params_and_failures(mode):
     """Per-slot thresholds / min-ingress and fail-nodes (failed peers burn fanout slots)."""
     run_parity(180, [1, 3, 5, 9], 42, p=0.03, mode=mode, thr=[0.0, 0.15, 0.4, 1.0], mi=[0, 2, 3, 1],
@@ -250,7 +250,8 @@ def test_rotation_round_sequence_and_deferred_clear():
 
 
 @pytest.mark.parametrize("mode,narrow", [(gs.GS_BFS_LEVEL, False), (gs.GS_BFS_BINNED, False),
-                                         (gs.GS_BFS_LEVEL, True), (gs.GS_BFS_BINNED, True)])
+                                         (gs.GS_BFS_LEVEL, True), (gs.GS_BFS_BINNED, True),
+                                         (gs.GS_BFS_MULTI, False), (gs.GS_BFS_MULTI, True)])
 def test_fused_round_matches_steps(mode, narrow):
     """gs_round's step-kernel path (consume + prune + apply of gs_consume_g.hip: register,
     wave and serial consume paths, register and wave prune paths) == the step-by-step
@@ -585,7 +586,7 @@ def test_c4_sweep_slots_1m():
     thr = [0.15] * 5 + [0.05 * (j + 1) for j in range(8)]
     S = len(fr)
     engs = [gs.Engine(st, S, seed=C2_SEED, rotation_probability=0.013333, bfs_mode=m)
-            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED)]
+            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI)]
     for e in engs:
         e.set_slots([origin] * S, 2, thr)
         e.init_active_sets()
@@ -593,22 +594,27 @@ def test_c4_sweep_slots_1m():
     for r in range(22):
         for e in engs:
             e.round(r, record=True)
-    a, b = engs
-    sa, sb = a.summaries(), b.summaries()
-    np.testing.assert_array_equal(sa, sb)
+    a = engs[0]
+    sa = a.summaries()
+    for b in engs[1:]:
+        np.testing.assert_array_equal(sa, b.summaries())
     for k in range(S):
         fa = a.failed(k)
         assert int(fa.sum()) == int(fr[k] * n)  # floor(f * N) nodes fail (gossip.rs:756-771)
-        np.testing.assert_array_equal(fa, b.failed(k))
         ha = _invariants(a, k, n, sa[-1, k], failed=fa) if k in (0, 4, 5, 12) else a.hops(k)
-        np.testing.assert_array_equal(ha, b.hops(k))
-        for x, y in zip(a.counters(k), b.counters(k)):
-            np.testing.assert_array_equal(x, y)
-        for x, y in zip(a.accumulators(k), b.accumulators(k)):
-            np.testing.assert_array_equal(x, y)
+        ca, aa = a.counters(k), a.accumulators(k)
+        for b in engs[1:]:
+            np.testing.assert_array_equal(fa, b.failed(k))
+            np.testing.assert_array_equal(ha, b.hops(k))
+            for x, y in zip(ca, b.counters(k)):
+                np.testing.assert_array_equal(x, y)
+            for x, y in zip(aa, b.accumulators(k)):
+                np.testing.assert_array_equal(x, y)
     for k in (0, 12):
-        for x, y in zip(a.inbound(k, cap=32 * n), b.inbound(k, cap=32 * n)):
-            np.testing.assert_array_equal(x, y)
+        ia = a.inbound(k, cap=32 * n)
+        for b in engs[1:]:
+            for x, y in zip(ia, b.inbound(k, cap=32 * n)):
+                np.testing.assert_array_equal(x, y)
     # the threshold slots share origin, trajectory and caches until they prune: at the
     # first prune round a higher threshold keeps more inbound stake, so prunes do not grow
     pr = sa["prunes"][:, 5:].astype(np.int64)
@@ -625,21 +631,61 @@ def test_c3_widest_rows_100k():
     n = 100_000
     st = eb.synth.power_law_stakes(n)
     engs = [gs.Engine(st, 2, seed=C2_SEED, active_set_size=27, rotation_probability=0.013333, bfs_mode=m)
-            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED)]
+            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI)]
     for e in engs:
         e.set_slots([int(np.argmax(st)), n // 3], 2, 0.15)
         e.init_active_sets()
         for r in range(4):
             e.round(r, record=True)
-    a, b = engs
+    a = engs[0]
     peers, lens = a.active_sets()
     assert (lens == 27).all()
     srt = np.sort(peers, axis=2)
     assert (np.diff(srt.astype(np.int64), axis=2) != 0).all()
-    np.testing.assert_array_equal(peers, b.active_sets()[0])
     sa = a.summaries()
-    np.testing.assert_array_equal(sa, b.summaries())
+    for b in engs[1:]:
+        np.testing.assert_array_equal(peers, b.active_sets()[0])
+        np.testing.assert_array_equal(sa, b.summaries())
     for k in range(2):
-        np.testing.assert_array_equal(_invariants(a, k, n, sa[-1, k]), b.hops(k))
-        for x, y in zip(a.inbound(k, cap=32 * n), b.inbound(k, cap=32 * n)):
+        ha = _invariants(a, k, n, sa[-1, k])
+        ia = a.inbound(k, cap=32 * n)
+        for b in engs[1:]:
+            np.testing.assert_array_equal(ha, b.hops(k))
+            for x, y in zip(ia, b.inbound(k, cap=32 * n)):
+                np.testing.assert_array_equal(x, y)
+
+
+def test_multi_bfs_groups_and_entries():
+    """The multi-source BFS with 70 slots (three slot groups of <= 32) whose origins have
+    different buckets (so a node's slots split over several entries k = min(bucket[u],
+    bucket[origin])), failures, per-slot thresholds, 30 rounds through a prune wave:
+    equal to the level BFS in every summary, hop table, counter, cache and accumulator."""
+    n, S = 3000, 70
+    pks, st = eb.synth.network(n)
+    engs = [gs.Engine(st, S, seed=9, rotation_probability=0.03, bfs_mode=m) for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_MULTI)]
+    origins = [(k * 131 + 7) % n for k in range(S - 6)] + [5, 5, 5, 77, 77, 77]  # shared origins too
+    fr = [0.0, 0.1, 0.0, 0.3] * (S // 4) + [0.0] * (S % 4)
+    for e in engs:
+        e.set_slots(origins, [k % 4 for k in range(S)], [0.05 * (k % 7) for k in range(S)])
+        e.init_active_sets()
+        e.fail_nodes(fr)
+    for r in range(30):
+        for e in engs:
+            e.round(r, record=r >= 4)
+    a, b = engs
+    np.testing.assert_array_equal(a.summaries(), b.summaries())
+    assert int(a.summaries()["prunes"].sum()) > 0
+    for k in (0, 17, 31, 32, 50, 63, 64, 66, 69):
+        np.testing.assert_array_equal(a.hops(k), b.hops(k))
+        np.testing.assert_array_equal(a.pruned_all(k), b.pruned_all(k))
+        for x, y in zip(a.counters(k), b.counters(k)):
+            np.testing.assert_array_equal(x, y)
+        for x, y in zip(a.caches(k), b.caches(k)):
+            np.testing.assert_array_equal(x, y)
+        for x, y in zip(a.accumulators(k), b.accumulators(k)):
+            np.testing.assert_array_equal(x, y)
+    for e in engs:
+        e.run_gossip()
+    for k in (0, 40, 69):
+        for x, y in zip(a.inbound(k), b.inbound(k)):
             np.testing.assert_array_equal(x, y)
