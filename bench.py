@@ -1,27 +1,45 @@
 #!/usr/bin/env python3
 """bench.py -- push-propagation edges/s on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], "C2"): a ~3,000-node synthetic power-law
-stake network, ALL 3,000 origins batched as independent sims (slots) of one
-engine, rotation probability 0.01, push fanout 6, active-set size 12. A step is
+Headline workload (BASELINE.json configs[1], "C2"): a ~3,000-node synthetic
+power-law stake network, ALL 3,000 origins batched as independent sims (slots) of
+one engine, rotation probability 0.01, push fanout 6, active-set size 12. A step is
 one full gossip iteration for every slot (gossip_main.rs:449-564: run_gossip ->
 consume -> send_prunes -> prune_connections -> chance_to_rotate -> the
-measured-round statistics), with all inputs resident in HBM.
+measured-round statistics), with all inputs resident in HBM. The K timed steps are
+rounds [W, W+K) of the simulation (W = --warmup); `config.rounds` says which, and
+`steady_state` times rounds [60, 160) of the same engine (past the first prune
+waves, where pushes per origin-round settle near 3N).
 
-value = pushes to non-failed peers over all slots and ranks / wall time of the
-K timed steps (max over ranks). Multi-GPU: one process per GPU; each rank runs
-its own 3,000 origin-sims with seed + rank (independent sims, no data-path
-collective) => "scaling": "weak". torch.distributed (gloo) is used only for the
-barrier and the max/sum of the timing scalars.
+value = pushes to non-failed peers over all slots and ranks / wall time of the K
+timed steps (max over ranks).
 
-roofline: the propagation kernel (BFS) with SURVEY.md 8(d) algorithmic bytes
-B_prop = V*(4*ASZ + 5) + 8*E per origin-round, divided by that kernel's summed
-duration measured with hipEvents on the engine stream over the timed steps.
+Multi-GPU (one process per GPU): by default every rank runs its own 3,000-origin
+network (seed + rank, "scaling": "weak"). With --shard-origins the ranks split the
+SAME 3,000 origins of ONE network (rank r takes origins [r*S/K, (r+1)*S/K)), the
+run is "strong" scaling, and rank 0 checks the gathered per-round summaries of
+every origin against the same origins run on one engine when --check-shard is set.
+torch.distributed carries only the barrier, the timing max/sum and the summary
+gather.
+
+roofline: the dominant kernel (k_round_wg) with SURVEY.md 8(d) algorithmic bytes
+per launch, divided by that kernel's average duration measured with hipEvents on
+the engine stream over the timed steps; `traffic` = HBM bytes per launch from the
+committed rocprofv3 --pmc summary of the SAME round window (profiles/r02/), or null.
 cpu_baseline: the oracle (reference-structure C++ restatement: maps keyed by
-32-byte pubkeys, one origin at a time, single core) timed on this host on a
-bounded sample of the same workload.
+32-byte pubkeys, one origin per sim) on all host cores (independent origin-sims
+dealt over std::threads) on a bounded sample of the same workload;
+cpu_baseline_1core: the same code on one core.
+Secondary legs at N = 1 (reported beside `value`, never part of it):
+  c4: BASELINE C4 as configured -- 1M-node network, origin rank 1, the fail-nodes
+      sweep (0.1..0.5, when-to-fail 0) and the prune-stake-threshold sweep
+      (0.05..0.40) as 13 slots of one engine; the propagation path's B_prop
+      fraction of HBM peak is the north-star figure.
+  c3: BASELINE C3's per-GPU share -- 100k nodes, active-set-size sweep values 12
+      and 20 (sims 0 and 8 of 16 dealt over 8 GPUs), one engine per value.
 """
 import argparse
+import glob
 import importlib.util
 import json
 import os
@@ -43,22 +61,42 @@ def load_pkg():
     return mod
 
 
-def pmc_traffic(kernel, nodes, slots):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary of
-    this same workload (scripts/pmc.sh + scripts/pmc_summary.py), or None."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{kernel}_{nodes}x{slots}.json")),
-                       reverse=True):
+def pmc_traffic(tag):
+    """HBM bytes per launch from the newest committed rocprofv3 --pmc summary named
+    profiles/r*/pmc_<tag>.json (scripts/pmc.sh + scripts/pmc_summary.py), or None."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{tag}.json")), reverse=True):
         with open(path) as f:
             d = json.load(f)
         return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
 
 
-def cpu_baseline(pks, stakes, args, budget_s):
-    """Oracle (port of the reference path) on host cores: one origin-sim, rounds until the budget."""
+def roofline(bytes_total, ms, launches, kernel, model, traffic_tag=None):
+    if ms <= 0:
+        return None
+    ach = bytes_total / (ms * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic(traffic_tag) if traffic_tag else (None, None)
+    return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc, "kernel": kernel,
+            "bytes_model": model, "bytes_per_launch": round(bytes_total / max(launches, 1)),
+            "avg_launch_us": round(ms * 1e3 / max(launches, 1), 2), "launches": launches}
+
+
+def b_prop(V, E, asz):
+    """V*(4*ASZ + 5) + 8*E per origin-round of the propagation kernel."""
+    return V * (4 * asz + 5) + 8 * E
+
+
+# ------------------------------------------------------------------ CPU baseline ----
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind as ob  # test infrastructure: used only as the baseline/checker here
+    return ob
+
+
+def cpu_baseline_1core(pks, stakes, args, budget_s):
+    """Oracle on one core: one origin-sim, rounds until the budget."""
+    ob = _oracle()
     sim = ob.Sim(ob.PHILOX, args.seed, pks, stakes, args.fanout)
     t0 = time.perf_counter()
     sim.init_philox(args.active_set_size)
@@ -71,7 +109,7 @@ def cpu_baseline(pks, stakes, args, budget_s):
                            rounds)
         rounds += 1
         el = time.perf_counter() - t0
-        if (el >= budget_s and rounds >= 3) or rounds >= args.warmup + args.steps:
+        if (el >= budget_s and rounds >= 3) or rounds >= 60:
             break
     return {"value": edges / el, "unit": "edges/s", "cores": 1, "kind": "port",
             "sample": f"1 origin-sim (origin rank 1) of the same {len(pks)}-node network, rounds 0..{rounds - 1} "
@@ -80,15 +118,47 @@ def cpu_baseline(pks, stakes, args, budget_s):
             "origin_rounds_per_s": rounds / el}
 
 
-def large_leg(gs, synth, args, nodes=1_000_000, slots=8, warmup=5, steps=20):
-    """SURVEY 8(d) C4-shaped secondary measurement (1 GPU): a 1M-node network, 8 origin
-    slots (independent sims, origins = node ids 0..7), the step-kernel round with the binned BFS. Reports the propagation path's
-    B_prop fraction of HBM peak (north-star target) and the whole round's rate."""
-    pks, stakes = synth.network(nodes)
-    eng = gs.Engine(stakes, slots, fanout=args.fanout, active_set_size=args.active_set_size,
-                    rotation_probability=args.rotation_probability, seed=args.seed, device=0, profile=True)
-    eng.set_slots(list(range(slots)), args.min_ingress, args.threshold)
+def cpu_baseline_all(pks, stakes, args, rounds=40):
+    """Oracle on all the host's cores: independent origin-sims (origins = node ids
+    0, 1, ... as in the GPU run) dealt over std::threads, rounds [0, rounds)."""
+    import ctypes as C
+    import numpy as np
+    ob = _oracle()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    n_sims = threads
+    f = ob.lib.or_bench_parallel
+    f.restype = C.c_uint64
+    f.argtypes = [C.c_uint64, C.c_char_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p, C.c_size_t,
+                  C.c_double, C.c_size_t, C.c_double, C.c_uint32, C.c_uint32, C.POINTER(C.c_double),
+                  C.POINTER(C.c_double)]
+    st = np.ascontiguousarray(stakes, dtype=np.uint64)
+    org = np.arange(n_sims, dtype=np.uint32) % len(pks)
+    ti, tr = C.c_double(), C.c_double()
+    edges = f(args.seed, ob.pk_blob(pks), st.ctypes.data, len(pks), args.fanout, args.active_set_size,
+              org.ctypes.data, n_sims, args.threshold, args.min_ingress, args.rotation_probability, rounds, threads,
+              C.byref(ti), C.byref(tr))
+    return {"value": edges / tr.value, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"{n_sims} origin-sims (origins = node ids 0..{n_sims - 1}) of the same {len(pks)}-node "
+                      f"network, rounds 0..{rounds - 1} each ({edges} pushes in {tr.value:.2f} s wall on {threads} "
+                      f"threads; active-set init {ti.value:.2f} s untimed); oracle/ reference-structure C++ "
+                      f"restatement, one std::thread per core",
+            "origin_rounds_per_s": n_sims * rounds / tr.value}
+
+
+# ------------------------------------------------------------------ secondary legs ----
+def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
+    """BASELINE C4 as configured on one GPU (13 sims as slots of one engine)."""
+    import numpy as np
+    stakes = synth.power_law_stakes(nodes)
+    origin = int(np.argmax(stakes))  # origin rank 1
+    fr = [0.1, 0.2, 0.3, 0.4, 0.5] + [0.0] * 8
+    thr = [args.threshold] * 5 + [round(0.05 * (j + 1), 2) for j in range(8)]
+    S = len(fr)
+    eng = gs.Engine(stakes, S, fanout=args.fanout, active_set_size=args.active_set_size,
+                    rotation_probability=0.013333, seed=args.seed, device=0, profile=True, bfs_mode=args.large_mode)
+    eng.set_slots([origin] * S, args.min_ingress, thr)
     eng.init_active_sets()
+    eng.fail_nodes(fr)  # when-to-fail 0: before the first BFS (gossip_main.rs:449-452)
     for r in range(warmup):
         eng.round(r, record=False)
     eng.sync()
@@ -101,28 +171,71 @@ def large_leg(gs, synth, args, nodes=1_000_000, slots=8, warmup=5, steps=20):
     summ = eng.summaries()
     E = float(summ["pushes"].astype("float64").sum())
     V = float(summ["visited"].astype("float64").sum())
-    b_ms, _ = eng.kernel_time("bfs")
+    fam = {k: eng.kernel_time(k)[0] for k in ("bfs", "consume", "rotate", "stats")}
     info = eng.info()
     eng.close()
-    b_prop = V * (4 * args.active_set_size + 5) + 8 * E
-    ach = b_prop / (b_ms * 1e-3) / 1e9 if b_ms > 0 else None
-    return {"workload": f"C4-shaped: {nodes}-node power-law network, {slots} origin slots, step-kernel round",
-            "bfs_mode": info["bfs_mode"], "steps": steps, "warmup": warmup,
+    mode = {2: "level", 3: "binned", 4: "multi"}.get(info["bfs_mode"], str(info["bfs_mode"]))
+    bp = b_prop(V, E, args.active_set_size)
+    return {"workload": f"C4: {nodes}-node power-law network, origin rank 1, fail-nodes 0.1..0.5 (when-to-fail 0) + "
+                        f"prune-stake-threshold 0.05..0.40: {S} sims as slots of one engine",
+            "bfs_mode": mode, "rounds": [warmup, warmup + steps], "ms_per_step": dt / steps * 1e3,
+            "edges_per_s": E / dt, "origin_rounds_per_s": S * steps / dt,
+            "pushes_per_origin_round": E / (S * steps),
+            "us_per_round": {k: round(v * 1e3 / steps, 1) for k, v in fam.items()},
+            "bfs_roofline": roofline(bp, fam["bfs"], steps, f"BFS ({mode}: expand/apply per level + gather)",
+                                     "B_prop (SURVEY 8d), summed over slots", f"bfs_{mode}_c4")}
+
+
+def c3_leg(gs, synth, args, nodes=100_000, warmup=5, steps=20):
+    """BASELINE C3's share of one GPU: ASZ 12 and 20 (sims 0 and 8 of the 16-sim sweep
+    dealt over 8 GPUs), one engine (one slot) per value, origin rank 1."""
+    import numpy as np
+    stakes = synth.power_law_stakes(nodes)
+    origin = int(np.argmax(stakes))
+    engs = []
+    for asz in (12, 20):
+        e = gs.Engine(stakes, 1, fanout=args.fanout, active_set_size=asz, rotation_probability=0.013333,
+                      seed=args.seed, device=0, profile=True, bfs_mode=args.large_mode)
+        e.set_slots([origin], args.min_ingress, args.threshold)
+        e.init_active_sets()
+        engs.append((asz, e))
+    for r in range(warmup):
+        for _, e in engs:
+            e.round(r, record=False)
+    for _, e in engs:
+        e.sync()
+        e.kernel_time_reset()
+    t0 = time.perf_counter()
+    for r in range(warmup, warmup + steps):
+        for _, e in engs:
+            e.round(r, record=True)
+    for _, e in engs:
+        e.sync()
+    dt = time.perf_counter() - t0
+    E = bp = b_ms = 0.0
+    for asz, e in engs:
+        s = e.summaries()
+        Ee = float(s["pushes"].astype("float64").sum())
+        Ve = float(s["visited"].astype("float64").sum())
+        E += Ee
+        bp += b_prop(Ve, Ee, asz)
+        b_ms += e.kernel_time("bfs")[0]
+        mode = {2: "level", 3: "binned", 4: "multi"}.get(e.info()["bfs_mode"])
+        e.close()
+    return {"workload": f"C3 per-GPU share: {nodes}-node network, active-set-size sweep values 12 and 20, one "
+                        f"engine each, origin rank 1", "bfs_mode": mode, "rounds": [warmup, warmup + steps],
             "ms_per_step": dt / steps * 1e3, "edges_per_s": E / dt,
-            "bfs_us_per_round": b_ms * 1e3 / steps,
-            "bfs_roofline": {"bound": "hbm", "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
-                             "bytes_model": "B_prop (SURVEY 8d)",
-                             "kernels": "k_bin_direct/k_bin_expand/k_bin_apply per level + k_bin_gather"}}
+            "bfs_roofline": roofline(bp, b_ms, 2 * steps, f"BFS ({mode})", "B_prop (SURVEY 8d)")}
 
 
+# ------------------------------------------------------------------------ main ----
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--nodes", type=int, default=3000)
-    ap.add_argument("--slots", type=int, default=0, help="origin slots per GPU (default: all nodes)")
+    ap.add_argument("--slots", type=int, default=0, help="origin slots (default: all nodes)")
     ap.add_argument("--fanout", type=int, default=6)
     ap.add_argument("--active-set-size", type=int, default=12)
     ap.add_argument("--rotation-probability", type=float, default=0.01)
@@ -130,16 +243,28 @@ def main():
     ap.add_argument("--min-ingress", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0x5EED0003)
     ap.add_argument("--bfs-mode", type=int, default=0)
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--large-mode", type=int, default=0, help="BFS mode of the c4/c3 legs (0 = AUTO)")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-steady", action="store_true")
     ap.add_argument("--split-round", action="store_true", help="step kernels instead of the one-kernel round")
-    ap.add_argument("--no-large", action="store_true", help="skip the 1M-node secondary leg")
+    ap.add_argument("--no-large", action="store_true", help="skip the c4 / c3 legs")
+    ap.add_argument("--only-large", action="store_true", help="run only the c4 / c3 legs (A/B of BFS modes)")
+    ap.add_argument("--shard-origins", action="store_true",
+                    help="ranks split the origins of ONE network (strong scaling) instead of one network each")
+    ap.add_argument("--check-shard", action="store_true",
+                    help="with --shard-origins: rank 0 re-runs all origins on one engine and compares")
     args = ap.parse_args()
 
     gs = load_pkg()          # loads libgossip_hip.so (and its HIP runtime) before torch, if torch is used at all
     gs.lib()
     import gossip_sim_amd.synth as synth
+
+    if args.only_large:
+        out = {"c4": c4_leg(gs, synth, args), "c3": c3_leg(gs, synth, args)}
+        print(json.dumps(out), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -163,11 +288,18 @@ def main():
         return float(t.item())
 
     pks, stakes = synth.network(args.nodes)
-    S = args.slots or args.nodes
+    S_all = args.slots or args.nodes
+    all_origins = [s % args.nodes for s in range(S_all)]
+    if args.shard_origins:
+        import gossip_sim_amd.sweep as sweep
+        lo, hi = sweep.shard_range(S_all, rank, world)
+        origins, seed = all_origins[lo:hi], args.seed
+    else:
+        origins, seed = all_origins, args.seed + rank
+    S = len(origins)
     eng = gs.Engine(stakes, S, fanout=args.fanout, active_set_size=args.active_set_size,
-                    rotation_probability=args.rotation_probability, seed=args.seed + rank, device=local_rank,
+                    rotation_probability=args.rotation_probability, seed=seed, device=local_rank,
                     bfs_mode=args.bfs_mode, profile=not args.no_profile, split_round=args.split_round)
-    origins = [s % args.nodes for s in range(S)]
     eng.set_slots(origins, args.min_ingress, args.threshold)
     eng.init_active_sets()
     for r in range(args.warmup):
@@ -195,30 +327,62 @@ def main():
     #   propagation  B_prop    = V*(4*ASZ + 5) + 8*E
     #   consume      B_consume = 5*E + 16*R        (R = receiving pairs = V - origins)
     #   statistics   B_stats   = 8 per (origin, node)
-    b_prop = V * (4 * asz + 5) + 8 * E
+    bp = b_prop(V, E, asz)
     R = V - S * args.steps
-    b_round = b_prop + 5 * E + 16 * R + 8.0 * args.nodes * S * args.steps
-    b_kernel = b_round if fused else b_prop
-    roof = None
-    if k_ms > 0:
-        achieved = b_kernel / (k_ms * 1e-3) / 1e9
-        kname = "k_round_wg" if fused else {gs.GS_BFS_WORKGROUP: "k_bfs_wg", gs.GS_BFS_LEVEL: "k_bfs_level",
-                                            gs.GS_BFS_BINNED: "k_bin_expand+k_bin_apply"}[eng.info()["bfs_mode"]]
-        traffic, tsrc = pmc_traffic(kname, args.nodes, S)
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-                "kernel": kname,
-                "bytes_model": "B_prop+B_consume+B_stats (SURVEY 8d)" if fused else "B_prop (SURVEY 8d)",
-                "bytes_per_launch": round(b_kernel / max(k_n, 1)), "avg_launch_us": round(k_ms * 1e3 / max(k_n, 1), 2),
-                "launches": k_n}
+    b_round = bp + 5 * E + 16 * R + 8.0 * args.nodes * S * args.steps
+    win = f"c2_r{args.warmup}-{args.warmup + args.steps - 1}"
+    if fused:
+        roof = roofline(b_round, k_ms, k_n, "k_round_wg", "B_prop+B_consume+B_stats (SURVEY 8d)",
+                        f"k_round_wg_{win}" if S == 3000 and world == 1 else None)
+    else:
+        roof = roofline(bp, k_ms, k_n, "BFS", "B_prop (SURVEY 8d)")
     phases = None
     if os.environ.get("GS_PHASE_PROFILE") == "1" and fused:  # workgroup-ms per k_round_wg phase
         names = ["init", "bfs", "csr_stats", "consume_prune", "heavy", "summary"]
         phases = {nm: round(eng.kernel_time("phase." + chr(65 + i))[0], 2) for i, nm in enumerate(names)}
-        phases["bfs_levels_per_slot_round"] = round(eng.kernel_time("phase.H")[0] * 1e5 / (S * args.steps), 2)
-        lv = eng.kernel_time("phase.H")[0] * 1e5
-        for i, nm in enumerate(["lvl_row_load_cyc", "lvl_push_cyc", "lvl_rest_iters_cyc", "lvl_barriers_cyc"]):
-            phases[nm] = round(eng.kernel_time("phase." + chr(73 + i))[0] * 1e5 / max(lv, 1), 1)  # per level
+    shard_check = None
+    if args.shard_origins and world > 1:
+        # every origin's per-round summaries, gathered rank-major, against one engine running all origins
+        import numpy as np
+        import gossip_sim_amd.sweep as sweep
+        full = sweep.gather_rows(dist, summ.view(np.uint8).reshape(args.steps, -1), S_all, world,
+                                 row_bytes=summ.dtype.itemsize)
+        if rank == 0 and args.check_shard:
+            ref = gs.Engine(stakes, S_all, fanout=args.fanout, active_set_size=asz,
+                            rotation_probability=args.rotation_probability, seed=args.seed, device=local_rank,
+                            bfs_mode=args.bfs_mode)
+            ref.set_slots(all_origins, args.min_ingress, args.threshold)
+            ref.init_active_sets()
+            for r in range(args.warmup + args.steps):
+                ref.round(r, record=r >= args.warmup)
+            want = ref.summaries().view(np.uint8).reshape(args.steps, -1)
+            ref.close()
+            shard_check = bool(np.array_equal(full, want))
+            if not shard_check:
+                raise SystemExit("origin-sharded summaries differ from the one-engine run")
+    steady = None
+    if not args.no_steady and world == 1 and args.warmup + args.steps <= 60:
+        for r in range(args.warmup + args.steps, 60):
+            eng.round(r, record=False)
+        eng.sync()
+        eng.kernel_time_reset()
+        n_before = eng.summaries().shape[0]
+        t1 = time.perf_counter()
+        for r in range(60, 160):
+            eng.round(r, record=True)
+        eng.sync()
+        dts = time.perf_counter() - t1
+        ss = eng.summaries()[n_before:]
+        Es = float(ss["pushes"].astype("float64").sum())
+        Vs = float(ss["visited"].astype("float64").sum())
+        ks_ms, ks_n = eng.kernel_time("round" if fused else "bfs")
+        bs = b_prop(Vs, Es, asz) + 5 * Es + 16 * (Vs - S * 100) + 8.0 * args.nodes * S * 100
+        steady = {"rounds": [60, 160], "value": Es / dts, "ms_per_step": dts / 100 * 1e3,
+                  "pushes_per_origin_round": Es / (S * 100),
+                  "roofline": roofline(bs if fused else b_prop(Vs, Es, asz), ks_ms, ks_n,
+                                       "k_round_wg" if fused else "BFS",
+                                       "B_prop+B_consume+B_stats (SURVEY 8d)" if fused else "B_prop (SURVEY 8d)",
+                                       "k_round_wg_c2_r60-159" if fused and S == 3000 else None)}
     out = {
         "metric": METRIC,
         "value": E_all / dt,
@@ -228,26 +392,33 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.shard_origins else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (deterministic Philox power-law stakes, SURVEY.md 8(d))",
         "config": {"workload": "C2: ~3,000-node power-law network, all origins batched, rotation-probability 0.01",
-                   "nodes": args.nodes, "origin_slots_per_gpu": S, "push_fanout": args.fanout,
-                   "active_set_size": asz, "rotation_probability": args.rotation_probability,
-                   "prune_stake_threshold": args.threshold, "min_ingress_nodes": args.min_ingress,
-                   "bfs_mode": eng.info()["bfs_mode"], "fused_round": fused,
-                   "parallelism": f"origin-sharded x{world}"},
-        "origin_rounds_per_s": S * args.steps * world / dt,
+                   "nodes": args.nodes, "origin_slots_per_gpu": S, "origins_total": S_all if args.shard_origins
+                   else S * world, "push_fanout": args.fanout, "active_set_size": asz,
+                   "rotation_probability": args.rotation_probability, "prune_stake_threshold": args.threshold,
+                   "min_ingress_nodes": args.min_ingress, "bfs_mode": eng.info()["bfs_mode"], "fused_round": fused,
+                   "rounds": [args.warmup, args.warmup + args.steps],
+                   "pushes_per_origin_round": E_all / (S * world * args.steps) if not args.shard_origins
+                   else E_all / (S_all * args.steps),
+                   "parallelism": f"origin-sharded x{world}" + (" (one network)" if args.shard_origins else "")},
+        "origin_rounds_per_s": (S_all if args.shard_origins else S * world) * args.steps / dt,
         "roofline": roof,
+        **({"steady_state": steady} if steady else {}),
+        **({"shard_check": shard_check} if shard_check is not None else {}),
         **({"phases_wg_ms": phases} if phases else {}),
         "cpu_baseline": None,
     }
     eng.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(pks, stakes, args, args.cpu_budget)
-    if rank == 0 and world == 1 and not args.no_large and args.nodes < 1_000_000:
-        out["large_1m"] = large_leg(gs, synth, args)
+        out["cpu_baseline"] = cpu_baseline_all(pks, stakes, args)
+        out["cpu_baseline_1core"] = cpu_baseline_1core(pks, stakes, args, args.cpu_budget)
+    if rank == 0 and world == 1 and not args.no_large:
+        out["c4"] = c4_leg(gs, synth, args)
+        out["c3"] = c3_leg(gs, synth, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

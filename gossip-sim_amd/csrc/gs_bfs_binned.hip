@@ -536,11 +536,14 @@ namespace gs {
 
 // Own-bucket entry rows (the entry a node uses for every origin whose bucket is at
 // least its own, push_active_set.rs:38-52): own[u] = peers[u][bucket[u]] and, in word
-// ASZP, hl | bucket << 16. Refreshed after init, rotation and entry uploads.
+// ASZP, hl | bucket << 16; with fcls (the multi-source BFS) words ASZP + 1 .. hold the
+// peers' failure classes, one byte each, so a row and its failure test are one line.
+// Refreshed after init, rotation, entry uploads and failures.
 template <int ASZP>
 __global__ void k_own_rows(const uint8_t* __restrict__ bucket, const uint32_t* __restrict__ peers,
                            const uint16_t* __restrict__ hl, const uint32_t* __restrict__ list,
-                           const uint32_t* __restrict__ count, uint32_t n_all, uint32_t ORW, uint32_t* __restrict__ own) {
+                           const uint32_t* __restrict__ count, uint32_t n_all, uint32_t ORW,
+                           const uint8_t* __restrict__ fcls, uint32_t* __restrict__ own) {
   const uint32_t n = count ? *count : n_all;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t u = list ? list[i] : i;
@@ -548,10 +551,17 @@ __global__ void k_own_rows(const uint8_t* __restrict__ bucket, const uint32_t* _
     const uint32_t ent = u * NB + b;
     uint32_t row[ASZP];
     load_row<ASZP>(peers + (size_t)ent * ASZP, row);
-    uint4* dst = reinterpret_cast<uint4*>(own + (size_t)u * ORW);
+    uint32_t* dst = own + (size_t)u * ORW;
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
 #pragma unroll
-    for (int q = 0; q < ASZP / 4; ++q) dst[q] = make_uint4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
-    dst[ASZP / 4] = make_uint4((uint32_t)hl[ent] | (b << 16), 0u, 0u, 0u);
+    for (int q = 0; q < ASZP / 4; ++q) d4[q] = make_uint4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+    dst[ASZP] = (uint32_t)hl[ent] | (b << 16);
+    if (fcls) {
+#pragma unroll
+      for (int q = 0; q < ASZP / 4; ++q)
+        dst[ASZP + 1 + q] = (uint32_t)fcls[row[4 * q]] | ((uint32_t)fcls[row[4 * q + 1]] << 8) |
+                            ((uint32_t)fcls[row[4 * q + 2]] << 16) | ((uint32_t)fcls[row[4 * q + 3]] << 24);
+    }
   }
 }
 
@@ -559,7 +569,7 @@ hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* coun
   if (!e.own) return hipSuccess;
   const uint32_t grid = (uint32_t)std::min<size_t>((e.N + 255) / 256, 2048);
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_own_rows<A>, dim3(grid), dim3(256), 0, e.st, e.bucket, e.peers,
-                                              e.hl, list, count, e.N, e.ASZP + 4, e.own));
+                                              e.hl, list, count, e.N, e.ORW, e.mv_fcls, e.own));
   return hipGetLastError();
 }
 
@@ -628,7 +638,7 @@ hipError_t launch_bfs_binned(Engine& e, bool record) {
   a.T = e.bin_T; a.pool = e.bin_pool; a.Lt = e.bin_Lt; a.binoff = e.bin_binoff;
   a.visbm = e.bin_vis;
   a.N = e.N; a.ASZ = e.ASZ; a.fanout = e.fanout; a.fc = e.fcap; a.capin = e.capin; a.Gmax = e.bin.Gmax;
-  a.PW = e.bin.PW; a.BS = e.bin.BS; a.nbins = e.bin.nbins; a.ORW = e.ASZP + 4; a.csr_cap = e.bin.csr_cap;
+  a.PW = e.bin.PW; a.BS = e.bin.BS; a.nbins = e.bin.nbins; a.ORW = e.ORW; a.csr_cap = e.bin.csr_cap;
   a.qmin = (e.prm.flags & GS_FLAG_BINNED_ALL_LEVELS) ? 1u : BIN_MIN_FRONTIER;
   if (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) a.csr_cap = 256;  // small tests reach the gather's direct placement
   a.PAIRS = e.PAIRS; a.pool_bin_cap = ((size_t)1 << e.bin.BS) * e.capin; a.record = record ? 1 : 0;

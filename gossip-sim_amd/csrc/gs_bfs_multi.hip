@@ -7,27 +7,35 @@
 // visited state is a slot mask per node (vis[N]); a frontier entry is (node u, entry
 // k, slot mask M): the slots in M first reached u at this level and all of them push
 // from u's entry k = min(bucket[u], bucket[origin]) (push_active_set.rs:38-52). Slots
-// that share u and k but not the entry are split into separate entries when u is
-// appended. Per BFS level:
+// that reach u at the same level through different entries become separate entries.
+// Prune masks and egress bytes are node-major ([node][slot]) in this mode: an entry
+// reads all its slots' masks in one line. Per BFS level:
 //
-//   expand (workgroup w owns frontier entries [w*PW, (w+1)*PW)): loads the entry's row
-//     (the compact own-bucket table when k = bucket[u]), takes per slot the first
-//     `fanout` unpruned non-origin ring slots (failed peers burn a slot, gossip.rs:
-//     527-541) and ORs the slot's bit into a per-ring-slot mask; every pushed-to peer w
-//     becomes ONE record (src u, w, slots) however many slots pushed there. Records
-//     are ranked per destination bin (2^BS nodes) with LDS atomics, staged sorted by
-//     bin and written as one contiguous run; T row [base, bin starts..., total].
-//   apply (one workgroup per bin, bins dealt to XCDs in contiguous ranges): ORs the
-//     level's records into an LDS copy of the bin's vis masks; new bits are first
-//     arrivals at hop d+1 (gossip.rs:594-600); new nodes are appended to the next
-//     frontier, one entry per distinct entry k.
-//   gather (after the last level, one workgroup per bin): the bin's records of every
-//     level as an LDS CSR by destination; per (slot, node): in-degree, the inbound
-//     records hop << 24 | src (gossip.rs:601-607) written as rows inb[c][pair]
-//     coalesced over nodes, and the hop (1 + the smallest pusher level; 0 at the
-//     origin, unreached = 0xFF).
+//   expand (workgroup w owns frontier entries [w*256, (w+1)*256)): loads the entry's
+//     row (the compact own-bucket table when k = bucket[u]) and its slots' masks, takes
+//     per slot the first `fanout` unpruned non-origin ring slots (failed peers burn a
+//     slot, gossip.rs:527-541) and ORs the slot's bit into a per-ring-slot mask; every
+//     pushed-to peer w becomes ONE record (src u, w, slots) however many slots pushed
+//     there. Records are ranked per coarse destination bin (2^BSC nodes) with LDS
+//     atomics, staged sorted by bin and written as one contiguous run; T row [base, bin
+//     starts..., total].
+//   apply (one workgroup per coarse bin, bins dealt to XCDs in contiguous ranges): ORs
+//     the level's records into an LDS copy of the bin's vis masks -- new bits are first
+//     arrivals at hop d+1 (gossip.rs:594-600) -- appends new nodes to the next frontier
+//     (one entry per distinct entry k) and the level's records to the bin's pool run.
+//   gather (after the last level, one workgroup per fine bin of 2^BSF nodes): the
+//     fine bin's records of every level (its coarse bin's pool runs, filtered) as an LDS
+//     CSR by destination; per (slot, node): in-degree, the inbound records
+//     hop << 24 | src (gossip.rs:601-607) as rows inb[c][pair] coalesced over nodes, and
+//     the hop (1 + the smallest pusher level; 0 at the origin; unreached = 0xFF).
 //
+// The level loop never stalls the GPU on the host: expand(d) writes its frontier size
+// to host-mapped memory and the host polls it two levels late (after an event).
 // Results equal k_bfs_level's: hops, in-degrees, inbound record sets, egress.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
 #include "gs_device.h"
 #include "gs_internal.h"
 
@@ -35,10 +43,10 @@ namespace gs {
 
 namespace {
 
-constexpr uint32_t MV_XT = 256;       // expand threads
-constexpr uint32_t MV_AT = 256;       // apply threads
+constexpr uint32_t MV_XT = 256;       // expand threads = frontier entries per expand workgroup
+constexpr uint32_t MV_AT = 1024;      // apply threads
 constexpr uint32_t MV_GT = 512;       // gather threads
-constexpr uint32_t MV_SEG = 1024;     // T rows per apply / gather chunk
+constexpr uint32_t MV_SEG = 1024;     // T rows per apply chunk
 constexpr uint32_t GT_OWN = 0, GT_NOBS = 25, GT_OBV = 26, GT_OBM = 58, GT_NSEED = 90, GT_SEED = 91, GT_S0 = 92,
                    GT_SG = 93;
 
@@ -47,24 +55,27 @@ struct MvArgs {
   const uint32_t* peers;
   const uint16_t* hl;
   const uint32_t* own;    // [N][ORW] own-bucket rows; word ASZP = hl | bucket << 16
-  const uint32_t* frank;
+  const uint8_t* fcls;    // [N] failure class: smallest i with fail rank < the i-th failure count
+  const uint8_t* fk;      // [S] failure class index of the slot's count (0: no failures)
   const uint32_t* origin;
-  const uint32_t* nfail;
-  const uint32_t* mask;
+  const uint32_t* mask;   // node-major [N][SP]
   const uint32_t* gt;     // this group's table (GT_WORDS words)
   uint8_t* hops;
   uint32_t* cnt;
   uint32_t* inb;
-  uint8_t* egress;
+  uint8_t* egress;        // node-major [N][SP]
   uint32_t* err;
   uint32_t* vis;          // [N] slot masks reached
   uint32_t* lvl;          // [256] frontier entries per level
-  uint32_t* tb;           // [257] first T row of level d
-  uint32_t* T;            // [rows][TW]
-  unsigned long long* area;
-  uint32_t* ctr;          // [0] records used in area
-  uint32_t N, ASZ, fanout, capin, s0, Sg, UB, BS, nbins, TW, PW, ORW, any_fail, gcap;
-  size_t PAIRS, area_cap, rows_cap, q_cap;
+  uint32_t* hlvl;         // host-mapped [256]: expand(d) writes lvl[d] here
+  uint32_t* T;            // [rows_cap][TW] rows of the current level
+  unsigned long long* area;  // records of the current level
+  uint32_t* ctr;          // [0] records used in area (this level)
+  unsigned long long* pool;  // [nbf][pcap] records of the round, per fine bin, level runs
+  uint32_t* pused;        // [nbf] records in each fine bin's pool region
+  uint2* Lt;              // [256][nbf] (pool start, count) of fine bin f at level d
+  uint32_t N, SP, ASZ, fanout, capin, s0, Sg, UB, BSC, BSF, nbc, nbf, TW, ORW, any_fail, gcap;
+  size_t PAIRS, area_cap, rows_cap, q_cap, pcap;
 };
 
 __device__ inline uint32_t mv_xcd_bin(uint32_t i, uint32_t nbins) {
@@ -100,98 +111,139 @@ __device__ inline uint32_t mv_block_scan(uint32_t* h, uint32_t n, uint32_t* wsum
 __host__ __device__ inline size_t mv_hist_bytes(uint32_t nbins) { return 4 * (size_t)((nbins + 17 + 1) & ~1u); }
 
 // --------------------------------------------------------------- expand ----
-template <int ASZP, int XPT>
+constexpr uint32_t MV_SG4 = 7;  // slot quads per group (GW <= 28)
+
+// Words of an own-bucket row in the multi-source BFS: the ring, hl | bucket << 16, the
+// peers' failure classes (one byte each), padded to 16 bytes.
+template <int ASZP>
+constexpr int mv_orw() { return ((ASZP + 1 + ASZP / 4) + 3) & ~3; }
+
+// One frontier entry (node u, entry k, slot mask M): the pushed-to ring slots of every
+// slot in M (PushActiveSet::get_nodes(..).take(fanout), gossip.rs:527-541: unpruned,
+// not the origin, failed peers burn their slot) as per-ring-slot slot masks acc[s], and
+// each slot's egress byte. Slots whose mask is empty, that have no failures and share
+// the group's first origin push the same set: it is computed once.
+template <int ASZP>
+__device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const uint32_t* sorg, const uint32_t* sfk,
+                                       uint32_t (&row)[ASZP], uint32_t (&acc)[ASZP], uint32_t& u) {
+  constexpr int TQ = (mv_orw<ASZP>() - ASZP) / 4;
+  u = ent.x & 0xFFFFFFu;
+  const uint32_t k = ent.x >> 24, M = ent.y;
+  if (GS_OOB(u, a.N, a.err, "multi frontier node")) u = 0;
+  const uint32_t nq = (a.Sg + 3) >> 2;
+  // the row (with its failure classes) and every slot quad's masks: independent loads
+  const uint32_t* orow = a.own + (size_t)u * a.ORW;
+  load_row<ASZP>(orow, row);
+  uint32_t tail[4 * TQ];
+  {
+    const uint4* t4 = reinterpret_cast<const uint4*>(orow + ASZP);
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) {
+      const uint4 x = t4[q];
+      tail[4 * q] = x.x; tail[4 * q + 1] = x.y; tail[4 * q + 2] = x.z; tail[4 * q + 3] = x.w;
+    }
+  }
+  uint4 m4[MV_SG4];
+  const uint4* mq = reinterpret_cast<const uint4*>(a.mask + (size_t)u * a.SP + a.s0);
+#pragma unroll
+  for (uint32_t q = 0; q < MV_SG4; ++q) m4[q] = (q < nq && ((M >> (4 * q)) & 0xFu)) ? mq[q] : make_uint4(0, 0, 0, 0);
+  uint32_t hv = tail[0] & 0xFFFFu;
+  uint32_t fc[ASZP];
+  if ((tail[0] >> 16) == k) {
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) fc[s] = (tail[1 + s / 4] >> (8 * (s % 4))) & 0xFFu;
+  } else {  // an origin of lower bucket: entry min(bucket[u], bucket[origin])
+    const uint32_t ent_i = u * NB + k;
+    hv = a.hl[ent_i];
+    load_row<ASZP>(a.peers + (size_t)ent_i * ASZP, row);
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) fc[s] = a.any_fail ? a.fcls[row[s]] : 0xFFu;
+  }
+  const uint32_t head = hv & 0xFF, len = hv >> 8;
+  const uint32_t org0 = sorg[0];
+  uint32_t tk0 = 0, msh = 0;
+  bool have0 = false;
+  uint8_t* eg = a.egress + (size_t)u * a.SP + a.s0;
+#pragma unroll
+  for (uint32_t q = 0; q < MV_SG4; ++q) {
+    if (q >= nq) break;
+    const uint32_t mq4 = (M >> (4 * q)) & 0xFu;
+    if (!mq4) continue;
+    uint32_t egw = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) {
+      const uint32_t j = 4 * q + t;
+      if (!((mq4 >> t) & 1u)) continue;
+      const uint32_t pm = t == 0 ? m4[q].x : t == 1 ? m4[q].y : t == 2 ? m4[q].z : m4[q].w;
+      const uint32_t f = sfk[j];
+      uint32_t tk;
+      if (pm == 0 && f == 0 && sorg[j] == org0) {  // the shared push set
+        if (!have0) {
+          tk0 = taken_slots<ASZP>(row, head, len, a.ASZ, 0u, org0, a.fanout);
+          have0 = true;
+        }
+        tk = tk0;
+        msh |= 1u << j;
+      } else {
+        tk = taken_slots<ASZP>(row, head, len, a.ASZ, pm, sorg[j], a.fanout);
+        if (f) {  // failed peers burn their fanout slot (gossip.rs:538-541)
+#pragma unroll
+          for (int s = 0; s < ASZP; ++s)
+            if (fc[s] <= f) tk &= ~(1u << s);
+        }
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s) acc[s] |= ((tk >> s) & 1u) << j;
+      }
+      egw |= (uint32_t)__popc(tk) << (8 * t);
+    }
+    if (mq4 == 0xFu) {
+      *reinterpret_cast<uint32_t*>(eg + 4 * q) = egw;  // SP and s0 are multiples of 4
+    } else {
+#pragma unroll
+      for (uint32_t t = 0; t < 4; ++t)
+        if ((mq4 >> t) & 1u) eg[4 * q + t] = (uint8_t)(egw >> (8 * t));
+    }
+  }
+  if (msh) {
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s)
+      if ((tk0 >> s) & 1u) acc[s] |= msh;
+  }
+}
+
+template <int ASZP>
 __global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, const uint2* __restrict__ qcur) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t sorg[32], snf[32], sbase;
+  __shared__ uint32_t sorg[32], sfk[32], sbase;
   const uint32_t qn = a.lvl[d];
-  const uint32_t tb = a.tb[d];
-  constexpr uint32_t PW = MV_XT * XPT;
-  const uint32_t G = (qn + PW - 1) / PW;
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.tb[d + 1] = tb + G;  // read by apply(d+1) and the gather
-  if (qn == 0) return;
-  if ((size_t)tb + G > a.rows_cap) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.hlvl[d] = qn;  // the host's termination poll
+  const uint32_t G = (qn + MV_XT - 1) / MV_XT;
+  if (blockIdx.x >= G) return;  // idle workgroups leave before any setup
+  if (G > a.rows_cap) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.err, ERR_MV_CAP);
     return;
   }
-  const uint32_t tid = threadIdx.x, nb = a.nbins, BS = a.BS, UB = a.UB, BPm = (1u << BS) - 1;
+  const uint32_t tid = threadIdx.x, nb = a.nbc, BSC = a.BSC, UB = a.UB, BPm = (1u << BSC) - 1;
   if (tid < a.Sg) {
     sorg[tid] = a.origin[a.s0 + tid];
-    snf[tid] = a.nfail[a.s0 + tid];
+    sfk[tid] = a.fk[a.s0 + tid];
   }
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);  // [nb] + scan words
-  unsigned long long* stage = reinterpret_cast<unsigned long long*>(smem + mv_hist_bytes(nb));  // [PW * ASZP]
-  __syncthreads();
+  unsigned long long* stage = reinterpret_cast<unsigned long long*>(smem + mv_hist_bytes(nb));  // [MV_XT * ASZP]
   for (uint32_t w = blockIdx.x; w < G; w += gridDim.x) {
     for (uint32_t i = tid; i < nb; i += MV_XT) hist[i] = 0;
     __syncthreads();
-    uint32_t row[XPT][ASZP], acc[XPT][ASZP], uu[XPT];
+    uint32_t row[ASZP], acc[ASZP], u = 0;
 #pragma unroll
-    for (int j = 0; j < XPT; ++j) {
-      const uint32_t i = w * PW + j * MV_XT + tid;
-      uu[j] = 0;
+    for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
+    const uint32_t i = w * MV_XT + tid;
+    if (i < qn) mv_expand_entry<ASZP>(a, qcur[i], sorg, sfk, row, acc, u);
+    // every LDS atomic after every load: each record's rank within its coarse bin
+    uint32_t rk[ASZP];
 #pragma unroll
-      for (int s = 0; s < ASZP; ++s) { row[j][s] = 0; acc[j][s] = 0; }
-      if (i >= qn) continue;
-      const uint2 ent = qcur[i];
-      uint32_t u = ent.x & 0xFFFFFFu;
-      const uint32_t k = ent.x >> 24, M = ent.y;
-      if (GS_OOB(u, a.N, a.err, "multi frontier node")) continue;
-      uu[j] = u;
-      const uint32_t* orow = a.own + (size_t)u * a.ORW;
-      load_row<ASZP>(orow, row[j]);
-      const uint32_t meta = orow[ASZP];
-      uint32_t hv = meta & 0xFFFFu;
-      if ((meta >> 16) != k) {  // an origin of lower bucket: entry min(bucket[u], bucket[origin])
-        const uint32_t ent_i = u * NB + k;
-        hv = a.hl[ent_i];
-        load_row<ASZP>(a.peers + (size_t)ent_i * ASZP, row[j]);
-      }
-      const uint32_t head = hv & 0xFF, len = hv >> 8;
-      uint32_t fr[ASZP];
-      if (a.any_fail) {
-#pragma unroll
-        for (int s = 0; s < ASZP; ++s) fr[s] = a.frank[row[j][s]];
-      }
-      // slot masks four at a time: the loads issue back to back
-      for (uint32_t mm = M; mm;) {
-        uint32_t jj[4], pm[4];
-        int nq = 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          jj[t] = 0;
-          pm[t] = 0;
-          if (mm) {
-            jj[t] = __ffs(mm) - 1;
-            mm &= mm - 1;
-            pm[t] = a.mask[(size_t)(a.s0 + jj[t]) * a.N + u];
-            nq = t + 1;
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          if (t >= nq) break;
-          uint32_t tk = taken_slots<ASZP>(row[j], head, len, a.ASZ, pm[t], sorg[jj[t]], a.fanout);
-          const uint32_t nf = snf[jj[t]];
-          if (nf) {  // failed peers burn their fanout slot (gossip.rs:538-541)
-#pragma unroll
-            for (int s = 0; s < ASZP; ++s)
-              if (((tk >> s) & 1u) && fr[s] < nf) tk &= ~(1u << s);
-          }
-          a.egress[(size_t)(a.s0 + jj[t]) * a.N + u] = (uint8_t)__popc(tk);
-#pragma unroll
-          for (int s = 0; s < ASZP; ++s) acc[j][s] |= ((tk >> s) & 1u) << jj[t];
-        }
-      }
-    }
-    // every LDS atomic after every load: each record's rank within its bin
-    uint32_t rk[XPT][ASZP];
-#pragma unroll
-    for (int j = 0; j < XPT; ++j)
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) rk[j][s] = acc[j][s] ? atomicAdd(&hist[row[j][s] >> BS], 1u) : 0u;
+    for (int s = 0; s < ASZP; ++s) rk[s] = acc[s] ? atomicAdd(&hist[row[s] >> BSC], 1u) : 0u;
     __syncthreads();
-    uint32_t total = mv_block_scan(hist, nb, hist + nb);
+    const uint32_t total = mv_block_scan(hist, nb, hist + nb);
     if (tid == 0) {
       uint32_t base = atomicAdd(a.ctr, total);
       if ((size_t)base + total > a.area_cap) {
@@ -203,31 +255,29 @@ __global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, const
     __syncthreads();
     const uint32_t base = sbase;
     const bool ok = base != 0xFFFFFFFFu;
-    uint32_t* Tr = a.T + (size_t)(tb + w) * a.TW;
+    uint32_t* Tr = a.T + (size_t)w * a.TW;
     for (uint32_t b = tid; b < nb; b += MV_XT) Tr[1 + b] = ok ? hist[b] : 0u;
     if (tid == 0) {
       Tr[0] = ok ? base : 0u;
       Tr[1 + nb] = ok ? total : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < XPT; ++j)
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s)
-        if (acc[j][s]) {
-          const uint32_t wp = row[j][s];
-          stage[hist[wp >> BS] + rk[j][s]] = (unsigned long long)uu[j] | ((unsigned long long)(wp & BPm) << UB) |
-                                             ((unsigned long long)acc[j][s] << (UB + BS));
-        }
+    for (int s = 0; s < ASZP; ++s)
+      if (acc[s]) {
+        const uint32_t wp = row[s];
+        stage[hist[wp >> BSC] + rk[s]] = (unsigned long long)u | ((unsigned long long)(wp & BPm) << UB) |
+                                         ((unsigned long long)acc[s] << (UB + BSC));
+      }
     __syncthreads();
     if (ok)
-      for (uint32_t i = tid; i < total; i += MV_XT) a.area[base + i] = stage[i];
+      for (uint32_t r = tid; r < total; r += MV_XT) a.area[base + r] = stage[r];
     __syncthreads();
   }
 }
 
 // ---------------------------------------------------------------- apply ----
-__host__ __device__ inline size_t mv_apply_lds_bytes(uint32_t BS) {
-  return 4 * (2 * (size_t)MV_SEG + 1 + 2 * ((size_t)1 << BS) + 32 + GT_WORDS);
+__host__ __device__ inline size_t mv_apply_lds_bytes(uint32_t BSC) {
+  return 4 * (2 * (size_t)MV_SEG + 1 + 2 * ((size_t)1 << BSC) + 64 + GT_WORDS);
 }
 
 // Node v's new slots as frontier entries, one per distinct entry k: slots whose origin
@@ -257,50 +307,86 @@ __device__ inline uint32_t mv_parts(const uint32_t* gt, uint32_t v, uint32_t nw,
 __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint2* __restrict__ qnxt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t qn = a.lvl[d];
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[0] = 0;  // expand(d) is done with it; expand(d + 1) starts at 0
   if (qn == 0) return;
-  const uint32_t b = mv_xcd_bin(blockIdx.x, a.nbins);
-  if (b >= a.nbins) return;
-  const uint32_t tid = threadIdx.x, BS = a.BS, UB = a.UB, BP = 1u << BS, BPm = BP - 1;
-  const uint32_t G = (qn + a.PW - 1) / a.PW, tb = a.tb[d];
-  const uint32_t v0 = b << BS, nv = min(BP, a.N - v0);
+  const uint32_t c = mv_xcd_bin(blockIdx.x, a.nbc);
+  if (c >= a.nbc) return;
+  const uint32_t tid = threadIdx.x, BSC = a.BSC, UB = a.UB, BP = 1u << BSC, BPm = BP - 1;
+  const uint32_t G = (qn + MV_XT - 1) / MV_XT;
+  const uint32_t v0 = c << BSC, nv = min(BP, a.N - v0);
   uint32_t* pre = reinterpret_cast<uint32_t*>(smem);  // [MV_SEG + 1]
   uint32_t* sb = pre + MV_SEG + 1;                    // [MV_SEG]
   uint32_t* visL = sb + MV_SEG;                       // [BP]
   uint32_t* vis0 = visL + BP;                         // [BP]
-  uint32_t* ctl = vis0 + BP;                          // [32]
-  uint32_t* gt = ctl + 32;                            // [GT_WORDS]
-  for (uint32_t i = tid; i < GT_WORDS; i += MV_AT) gt[i] = a.gt[i];
-  for (uint32_t i = tid; i < nv; i += MV_AT) {
-    const uint32_t m = a.vis[v0 + i];
-    visL[i] = m;
-    vis0[i] = m;
-  }
-  __syncthreads();
+  uint32_t* ctl = vis0 + BP;                          // [64]: [0..15] scan words, [1] base, [8..23] counts
+  uint32_t* gt = ctl + 64;                            // [GT_WORDS]
+  // the level's records go to the pool run of their fine bin (2^BSF nodes): cursors per
+  // fine bin of this coarse bin, reserved once per wave per fine bin
+  const uint32_t FS = a.BSC - a.BSF, NF = 1u << FS, f0 = c << FS;
+  uint32_t* fcur = ctl + 32;  // [NF <= 16] records appended this level
+  if (tid < NF) fcur[tid] = 0;
+  bool loaded = false;  // vis is read only by bins that receive records at this level
   for (uint32_t c0 = 0; c0 < G; c0 += MV_SEG) {
     const uint32_t gc = min(MV_SEG, G - c0);
     for (uint32_t i = tid; i < gc; i += MV_AT) {
-      const uint32_t* Tr = a.T + (size_t)(tb + c0 + i) * a.TW;
-      const uint32_t st = Tr[1 + b];
-      pre[i] = Tr[2 + b] - st;  // bin starts are exclusive; Tr[1 + nbins] is the run's total
+      const uint32_t* Tr = a.T + (size_t)(c0 + i) * a.TW;
+      const uint32_t st = Tr[1 + c];
+      pre[i] = Tr[2 + c] - st;  // bin starts are exclusive; Tr[1 + nbc] is the run's total
       sb[i] = Tr[0] + st;
     }
     __syncthreads();
     const uint32_t ct = mv_block_scan(pre, gc, ctl);
+    if (ct == 0) continue;  // (uniform)
     if (tid == 0) pre[gc] = ct;
+    if (!loaded) {
+      for (uint32_t i = tid; i < GT_WORDS; i += MV_AT) gt[i] = a.gt[i];
+      for (uint32_t i = tid; i < nv; i += MV_AT) {
+        const uint32_t m = a.vis[v0 + i];
+        visL[i] = m;
+        vis0[i] = m;
+      }
+      loaded = true;
+    }
     __syncthreads();
-    for (uint32_t r = tid; r < ct; r += MV_AT) {
+    for (uint32_t r0 = 0; r0 < ct; r0 += MV_AT) {  // uniform trips: the fine-bin ballots need whole waves
+      const uint32_t r = r0 + tid;
+      const bool live = r < ct;
       uint32_t lo = 0, hi = gc;  // largest i with pre[i] <= r
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (pre[mid] <= r) lo = mid; else hi = mid;
       }
-      const unsigned long long rec = a.area[sb[lo] + (r - pre[lo])];
+      const unsigned long long rec = live ? a.area[sb[lo] + (r - pre[lo])] : 0ull;
       uint32_t vl = (uint32_t)(rec >> UB) & BPm;
-      if (GS_OOB(vl, nv, a.err, "multi record node")) vl = 0;
-      atomicOr(&visL[vl], (uint32_t)(rec >> (UB + BS)));
+      if (live && GS_OOB(vl, nv, a.err, "multi record node")) vl = 0;
+      if (live) atomicOr(&visL[vl], (uint32_t)(rec >> (UB + BSC)));
+      const uint32_t fb = live ? vl >> a.BSF : 0xFFFFu;
+      uint32_t pos = 0;
+      for (uint32_t k = 0; k < NF; ++k) {  // one LDS atomic per wave and fine bin
+        const uint64_t m = __ballot(fb == k);
+        if (!m) continue;
+        uint32_t base = 0;
+        const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
+        if (lane_id() == leader) base = atomicAdd(&fcur[k], (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, (int)leader);
+        if (fb == k) pos = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
+      }
+      if (live) {
+        const size_t pp = (size_t)a.pused[f0 + fb] + pos;
+        if (pp < a.pcap) a.pool[(size_t)(f0 + fb) * a.pcap + pp] = rec;
+      }
     }
     __syncthreads();
   }
+  __syncthreads();
+  if (tid < NF) {  // the level's run of each fine bin, for the gather
+    const uint32_t used = a.pused[f0 + tid], n = fcur[tid];
+    const bool over = (size_t)used + n > a.pcap;
+    if (over) atomicOr(a.err, ERR_MV_CAP);
+    a.Lt[(size_t)d * a.nbf + f0 + tid] = make_uint2(used, over ? 0u : n);
+    a.pused[f0 + tid] = over ? used : used + n;
+  }
+  if (!loaded) return;  // no records: no first arrivals in this bin
   // first arrivals (hop d + 1) become next-level entries, in node order
   uint32_t cntp = 0;
   for (uint32_t i = tid; i < nv; i += MV_AT) {
@@ -333,115 +419,211 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint2*
   }
 }
 
-// --------------------------------------------------------------- gather ----
+// ------------------------------------------------------------ small levels ----
+constexpr uint32_t MV_ST = 1024;     // threads of the small-level workgroup
+constexpr uint32_t MV_SMALL = 4096;  // frontier entries at most for a small level
 
-
-__host__ __device__ inline size_t mv_gather_fixed_bytes(uint32_t BS) {
-  return 4 * (2 * ((size_t)1 << BS) + 2 + 3 * (size_t)MV_SEG + 1 + 32 + 32);
+template <class T>
+__device__ inline T mv_ld(T* p) {  // device-scope load: lines updated by atomics elsewhere
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Walks the bin's records of levels [0, nlev) (T rows in level order); f(level, rec).
-template <class F>
-__device__ inline void mv_walk(const MvArgs& a, uint32_t b, uint32_t nlev, uint32_t* pre, uint32_t* sb, uint32_t* lv,
-                               uint32_t* ctl, F&& f) {
-  const uint32_t tid = threadIdx.x, TH = blockDim.x;
-  const uint32_t R = a.tb[nlev];
-  for (uint32_t c0 = 0; c0 < R; c0 += MV_SEG) {
-    const uint32_t gc = min(MV_SEG, R - c0);
-    for (uint32_t i = tid; i < gc; i += TH) {
-      const uint32_t r = c0 + i;
-      const uint32_t* Tr = a.T + (size_t)r * a.TW;
-      const uint32_t st = Tr[1 + b];
-      pre[i] = Tr[2 + b] - st;
-      sb[i] = Tr[0] + st;
-      uint32_t lo = 0, hi = nlev;  // level of row r: largest d with tb[d] <= r
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.tb[mid] <= r) lo = mid; else hi = mid;
-      }
-      lv[i] = lo;
+// Levels with at most MV_SMALL frontier entries run inside ONE workgroup, level after
+// level, with no launch between them: every entry is expanded (mv_expand_entry), each
+// record ORs its slots into vis with a device-scope atomic -- the atomic that sets a
+// slot's bit is that slot's first arrival (hop d + 1, gossip.rs:594-600) -- new bits
+// become next-level entries, and the record is appended to its fine bin's pool run
+// (one atomic per record: few records). Starts at level d0; stops at the first level
+// with no entries or more than MV_SMALL; writes (level, entries) to hstate.
+template <int ASZP>
+__global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2* __restrict__ q0,
+                                                    uint2* __restrict__ q1, uint32_t* __restrict__ hstate) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t snap[];  // [nbf] pool fill at level start
+  __shared__ uint32_t sorg[32], sfk[32], gt[GT_WORDS], cnt_s;
+  const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BPm = (1u << BSC) - 1;
+  if (tid < a.Sg) {
+    sorg[tid] = a.origin[a.s0 + tid];
+    sfk[tid] = a.fk[a.s0 + tid];
+  }
+  for (uint32_t i = tid; i < GT_WORDS; i += MV_ST) gt[i] = a.gt[i];
+  uint32_t d = d0, qn = a.lvl[d0];
+  while (qn > 0 && qn <= MV_SMALL && d < 254) {
+    uint2* qcur = (d & 1) ? q1 : q0;
+    uint2* qnxt = (d & 1) ? q0 : q1;
+    for (uint32_t f = tid; f < a.nbf; f += MV_ST) snap[f] = mv_ld(&a.pused[f]);
+    if (tid == 0) {
+      cnt_s = 0;
+      a.hlvl[d] = qn;
     }
     __syncthreads();
-    const uint32_t ct = mv_block_scan(pre, gc, ctl);
-    if (tid == 0) pre[gc] = ct;
-    __syncthreads();
-    for (uint32_t r = tid; r < ct; r += TH) {
-      uint32_t lo = 0, hi = gc;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pre[mid] <= r) lo = mid; else hi = mid;
+    for (uint32_t i0 = 0; i0 < qn; i0 += MV_ST) {
+      const uint32_t i = i0 + tid;
+      uint32_t row[ASZP], acc[ASZP], u = 0;
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
+      if (i < qn) mv_expand_entry<ASZP>(a, qcur[i], sorg, sfk, row, acc, u);
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        if (!acc[s]) continue;
+        const uint32_t w = row[s];
+        const uint32_t nw = acc[s] & ~atomicOr(&a.vis[w], acc[s]);
+        const uint32_t f = w >> a.BSF;
+        const uint32_t p = atomicAdd(&a.pused[f], 1u);
+        if (p < a.pcap)
+          a.pool[(size_t)f * a.pcap + p] = (unsigned long long)u | ((unsigned long long)(w & BPm) << UB) |
+                                           ((unsigned long long)acc[s] << (UB + BSC));
+        else
+          atomicOr(a.err, ERR_MV_CAP);
+        if (nw) {  // this thread's first arrivals at w (another thread may add more bits to w)
+          const uint32_t bw = a.bucket[w];
+          const uint32_t n = mv_parts(gt, w, nw, bw, nullptr, 0);
+          const uint32_t base = atomicAdd(&cnt_s, n);
+          if ((size_t)base + n <= a.q_cap) mv_parts(gt, w, nw, bw, qnxt, base);
+          else atomicOr(a.err, ERR_MV_CAP);
+        }
       }
-      f(lv[lo], a.area[sb[lo] + (r - pre[lo])]);
     }
     __syncthreads();
+    for (uint32_t f = tid; f < a.nbf; f += MV_ST)  // the level's pool run of every fine bin
+      a.Lt[(size_t)d * a.nbf + f] = make_uint2(snap[f], mv_ld(&a.pused[f]) - snap[f]);
+    qn = min(cnt_s, (uint32_t)a.q_cap);
+    ++d;
+    if (tid == 0) a.lvl[d] = qn;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    hstate[0] = d;
+    hstate[1] = qn;
   }
 }
 
+// --------------------------------------------------------------- gather ----
+constexpr uint32_t MV_GC = 12;        // records per gather thread kept in registers between the passes
+constexpr uint32_t MV_GLDS = 78 * 1024;  // gather LDS: two workgroups per CU
+
+__host__ __device__ inline size_t mv_gather_fixed_bytes(uint32_t BSF) {
+  return 4 * (256 + 257 + 2 * (((size_t)1 << BSF) + 1) + 16 + 32);
+}
+
+// After the last level, per fine bin: the bin's records of every level (its pool runs, in
+// level order) as an LDS CSR by destination, then per (slot, node) the in-degree, the
+// inbound rows and the hop, coalesced over nodes.
 __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t b = mv_xcd_bin(blockIdx.x, a.nbins);
-  if (b >= a.nbins) return;
-  const uint32_t tid = threadIdx.x, BS = a.BS, UB = a.UB, BP = 1u << BS, BPm = BP - 1, Sg = a.Sg;
-  const uint32_t v0 = b << BS, nv = min(BP, a.N - v0);
-  const unsigned long long um = (1ull << UB) - 1;
-  uint32_t* cn = reinterpret_cast<uint32_t*>(smem);  // [BP + 1] records per node -> CSR starts
+  const uint32_t f = mv_xcd_bin(blockIdx.x, a.nbf);
+  if (f >= a.nbf) return;
+  const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BSF = a.BSF, BP = 1u << BSF, BPm = BP - 1, Sg = a.Sg;
+  const uint32_t v0 = f << BSF;
+  if (v0 >= a.N) return;
+  const uint32_t nv = min(BP, a.N - v0);
+  const uint32_t um = (1u << UB) - 1;
+  uint32_t* rs = reinterpret_cast<uint32_t*>(smem);  // [256] pool start of level d's run
+  uint32_t* rp = rs + 256;                           // [257] records before level d's run
+  uint32_t* cn = rp + 257;                           // [BP + 1] records per node -> CSR starts
   uint32_t* cur = cn + BP + 1;                       // [BP + 1] placement cursors
-  uint32_t* pre = cur + BP + 1;                      // [MV_SEG + 1]
-  uint32_t* sb = pre + MV_SEG + 1;                   // [MV_SEG]
-  uint32_t* lv = sb + MV_SEG;                        // [MV_SEG]
-  uint32_t* ctl = lv + MV_SEG;                       // [32]
-  uint32_t* sorg = ctl + 32;                         // [32]
+  uint32_t* ctl = cur + BP + 1;                      // [16]
+  uint32_t* sorg = ctl + 16;                         // [32]
   uint32_t* keys = sorg + 32;                        // [gcap] hop << 24 | src
   uint32_t* msk = keys + a.gcap;                     // [gcap] slot masks
+  const unsigned long long* pool = a.pool + (size_t)f * a.pcap;
   for (uint32_t i = tid; i <= BP; i += MV_GT) cn[i] = 0;
   if (tid < Sg) sorg[tid] = a.origin[a.s0 + tid];
+  {  // the run table: thread d reads level d's (start, count); exclusive prefix of the counts
+    uint32_t n = 0;
+    if (tid < 256) {
+      rs[tid] = 0;
+      if (tid < nlev && a.lvl[tid]) {  // an empty level wrote no run
+        const uint2 L = a.Lt[(size_t)tid * a.nbf + f];
+        rs[tid] = L.x;
+        n = L.y;
+      }
+    }
+    const uint32_t incl = wave_incl_scan(n);
+    if ((tid & 63) == 63) ctl[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t off = incl - n;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) off += ctl[w];
+    if (tid < 256) rp[tid] = off;
+    if (tid == 255) rp[256] = off + n;
+  }
   __syncthreads();
-  // 1. records per destination node
-  mv_walk(a, b, nlev, pre, sb, lv, ctl, [&](uint32_t, unsigned long long rec) {
-    atomicAdd(&cn[(uint32_t)(rec >> UB) & BPm], 1u);
-  });
-  const uint32_t Etot = mv_block_scan(cn, BP, ctl);
-  if (tid == 0) cn[BP] = Etot;
+  const uint32_t Etot = rp[256];
+  // 1. count per node; the first MV_GC records of each thread stay in registers (key, mask, node)
+  uint32_t kc[MV_GC], mc[MV_GC], vc[MV_GC];
+  uint32_t lv = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < MV_GC; ++j) {
+    const uint32_t t = tid + j * MV_GT;
+    kc[j] = 0; mc[j] = 0; vc[j] = 0xFFFFFFFFu;
+    if (t < Etot) {
+      while (t >= rp[lv + 1]) ++lv;
+      const unsigned long long rec = pool[rs[lv] + (t - rp[lv])];
+      kc[j] = ((lv + 1) << 24) | ((uint32_t)rec & um);
+      mc[j] = (uint32_t)(rec >> (UB + BSC));
+      vc[j] = (uint32_t)(rec >> UB) & BPm;
+    }
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < MV_GC; ++j)
+    if (vc[j] != 0xFFFFFFFFu) atomicAdd(&cn[vc[j]], 1u);
+  for (uint32_t t = tid + MV_GC * MV_GT; t < Etot; t += MV_GT) {
+    while (t >= rp[lv + 1]) ++lv;
+    atomicAdd(&cn[(uint32_t)(pool[rs[lv] + (t - rp[lv])] >> UB) & BPm], 1u);
+  }
+  __syncthreads();
+  const uint32_t E2 = mv_block_scan(cn, BP, ctl);
+  if (tid == 0) cn[BP] = E2;
   __syncthreads();
   // 2. node ranges whose records fit the LDS CSR (one range unless the bin is heavy)
   bool over = false;
   for (uint32_t lo = 0; lo < nv;) {
-    uint32_t hi = lo;
     if (tid == 0) {
       uint32_t h = lo;
       while (h < nv && cn[h + 1] - cn[lo] <= a.gcap) ++h;
       if (h == lo) { atomicOr(a.err, ERR_MV_CAP); h = nv; }  // one node beyond the LDS CSR
-      ctl[16] = h;
+      ctl[15] = h;
     }
     __syncthreads();
-    hi = ctl[16];
+    const uint32_t hi = ctl[15];
     const uint32_t base = cn[lo];
     for (uint32_t i = lo + tid; i < hi; i += MV_GT) cur[i] = cn[i] - base;
     __syncthreads();
-    mv_walk(a, b, nlev, pre, sb, lv, ctl, [&](uint32_t d, unsigned long long rec) {
-      const uint32_t vl = (uint32_t)(rec >> UB) & BPm;
-      if (vl < lo || vl >= hi) return;
+#pragma unroll
+    for (uint32_t j = 0; j < MV_GC; ++j) {
+      const uint32_t vl = vc[j];
+      if (vl == 0xFFFFFFFFu || vl < lo || vl >= hi) continue;
       const uint32_t p = atomicAdd(&cur[vl], 1u);
-      if (p >= a.gcap) return;
-      keys[p] = ((d + 1) << 24) | (uint32_t)(rec & um);
-      msk[p] = (uint32_t)(rec >> (UB + BS));
-    });
+      if (p < a.gcap) { keys[p] = kc[j]; msk[p] = mc[j]; }
+    }
+    lv = 0;
+    for (uint32_t t = tid + MV_GC * MV_GT; t < Etot; t += MV_GT) {
+      while (t >= rp[lv + 1]) ++lv;
+      const unsigned long long rec = pool[rs[lv] + (t - rp[lv])];
+      const uint32_t vl = (uint32_t)(rec >> UB) & BPm;
+      if (vl < lo || vl >= hi) continue;
+      const uint32_t p = atomicAdd(&cur[vl], 1u);
+      if (p < a.gcap) {
+        keys[p] = ((lv + 1) << 24) | ((uint32_t)rec & um);
+        msk[p] = (uint32_t)(rec >> (UB + BSC));
+      }
+    }
+    __syncthreads();
     // 3. per (slot, node): in-degree, inbound rows, hop; coalesced over nodes
     for (uint32_t i = lo + tid; i < hi; i += MV_GT) {
       const uint32_t v = v0 + i, r0 = cn[i] - base, r1 = min(cn[i + 1] - base, a.gcap);
       for (uint32_t j = 0; j < Sg; ++j) {
         const size_t p = (size_t)(a.s0 + j) * a.N + v;
-        uint32_t c = 0, mh = 0xFFu;
-        for (uint32_t r = r0; r < r1; ++r) {
-          if (!((msk[r] >> j) & 1u)) continue;
+        uint32_t cc = 0, mh = 0xFFu;
+        for (uint32_t r = r0;; ++r, ++cc) {  // trip cc writes row cc: lanes store the same row together
+          while (r < r1 && !((msk[r] >> j) & 1u)) ++r;
+          if (r >= r1) break;
           const uint32_t key = keys[r];
-          if (c < a.capin) a.inb[(size_t)c * a.PAIRS + p] = key;
+          if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = key;
           mh = min(mh, key >> 24);
-          ++c;
         }
-        over |= c > a.capin;
-        a.cnt[p] = c;
-        a.hops[p] = (uint8_t)(v == sorg[j] ? 0u : (c ? mh : 0xFFu));
+        over |= cc > a.capin;
+        a.cnt[p] = cc;
+        a.hops[p] = (uint8_t)(v == sorg[j] ? 0u : (cc ? mh : 0xFFu));
       }
     }
     __syncthreads();
@@ -459,8 +641,22 @@ __global__ void k_mv_seed(MvArgs a, const uint2* __restrict__ seeds, uint32_t ns
   }
   if (i == 0) {
     a.lvl[0] = nseed;
-    a.tb[0] = 0;
     a.ctr[0] = 0;
+  }
+}
+
+// fcls[w] = smallest i (1-based) with frank[w] < T[i-1] over the ascending distinct
+// failure counts T[0..m); 255 when w fails in no slot.
+__global__ void k_mv_fcls(const uint32_t* __restrict__ frank, const uint32_t* __restrict__ T, uint32_t m, uint32_t N,
+                          uint8_t* __restrict__ fcls) {
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < N; w += gridDim.x * blockDim.x) {
+    const uint32_t fr = frank[w];
+    uint32_t lo = 0, hi = m;  // first i with T[i] > fr
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (T[mid] > fr) hi = mid; else lo = mid + 1;
+    }
+    fcls[w] = (uint8_t)(lo < m ? lo + 1 : 255);
   }
 }
 
@@ -474,26 +670,26 @@ static uint32_t ceil_log2(size_t x) {
 }
 
 void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g) {
+  (void)ASZP;
   g.UB = std::max(1u, ceil_log2(N));
-  g.BS = std::min(13u, std::max(6u, g.UB > 10 ? g.UB - 10 : 0u));
-  g.nbins = (N + (1u << g.BS) - 1) >> g.BS;
-  g.GW = std::min(32u, 64u - g.UB - g.BS);
-  g.XPT = ASZP <= 16 ? 2 : 1;
-  g.PW = MV_XT * g.XPT;
-  g.TW = g.nbins + 2;
+  g.BSC = std::min(13u, std::max(6u, g.UB > 8 ? g.UB - 8 : 0u));   // ~256 coarse bins
+  g.BSF = std::min(g.BSC, 10u);                                     // fine bins of <= 1,024 nodes
+  g.nbc = (N + (1u << g.BSC) - 1) >> g.BSC;
+  g.nbf = g.nbc << (g.BSC - g.BSF);
+  g.GW = std::min(28u, (64u - g.UB - g.BSC) & ~3u);
+  g.TW = g.nbc + 2;
   const size_t sg = std::min<size_t>(S, g.GW);
   g.q_cap = (size_t)N * std::min<size_t>(sg, 26) + 64;
-  const size_t hard = (size_t)N * sg * ASZ;  // every (slot, node) reached once, <= ASZ records each
-  g.area_cap = std::min(hard, std::max<size_t>((size_t)N * ASZ * 4, (size_t)1 << 29));
-  g.area_cap = std::min<size_t>(g.area_cap, 0xFFFFFFF0u);
-  const size_t rows_hard = (size_t)N * sg / g.PW + 260;
-  g.rows_cap = std::min(rows_hard, std::max<size_t>((size_t)N * 4 / g.PW + 260, ((size_t)1 << 30) / (4 * g.TW)));
-  const size_t lds_total = 160 * 1024;
-  g.gcap = (uint32_t)((lds_total - mv_gather_fixed_bytes(g.BS)) / 8);
+  g.area_cap = std::min<size_t>(g.q_cap * ASZ, 0xFFFFFFF0u);
+  g.rows_cap = (g.q_cap + MV_XT - 1) / MV_XT + 1;
+  const size_t rpn = (size_t)ASZ * std::min<size_t>(sg, 4) + 16;  // pool records per node (average over a bin)
+  g.pcap = ((size_t)1 << g.BSF) * rpn;
+  g.gcap = (uint32_t)((MV_GLDS - mv_gather_fixed_bytes(g.BSF)) / 8);
 }
 
 bool mv_supported(const MvGeom& g, uint32_t ASZP) {
-  return mv_hist_bytes(g.nbins) + (size_t)g.PW * ASZP * 8 <= 160 * 1024 && mv_apply_lds_bytes(g.BS) <= 160 * 1024;
+  return mv_hist_bytes(g.nbc) + (size_t)MV_XT * ASZP * 8 <= 160 * 1024 && mv_apply_lds_bytes(g.BSC) <= 160 * 1024 &&
+         g.GW >= 4;
 }
 
 // Host-side slot groups (contiguous ranges of <= GW slots) and their tables.
@@ -534,71 +730,123 @@ void mv_build_groups(Engine& e, const std::vector<uint32_t>& origins, const std:
   }
 }
 
+// After the failure counts change: per-slot failure classes and the per-node table.
+hipError_t mv_update_failures(Engine& e, const std::vector<uint32_t>& nf) {
+  if (e.bfs_mode != GS_BFS_MULTI) return hipSuccess;
+  std::vector<uint32_t> T;
+  for (uint32_t x : nf)
+    if (x) T.push_back(x);
+  std::sort(T.begin(), T.end());
+  T.erase(std::unique(T.begin(), T.end()), T.end());
+  if (T.size() > 254) return hipErrorInvalidValue;
+  std::vector<uint8_t> fk(e.S, 0);
+  for (uint32_t o = 0; o < e.S; ++o)
+    if (nf[o]) fk[o] = (uint8_t)(std::lower_bound(T.begin(), T.end(), nf[o]) - T.begin() + 1);
+  hipError_t r;
+  if ((r = hipMemcpyAsync(e.mv_fk, fk.data(), e.S, hipMemcpyHostToDevice, e.st))) return r;
+  if (!T.empty()) {
+    if ((r = hipMemcpyAsync(e.mv_thr, T.data(), T.size() * 4, hipMemcpyHostToDevice, e.st))) return r;
+    hipLaunchKernelGGL(k_mv_fcls, dim3(std::min<uint32_t>((e.N + 255) / 256, 4096)), dim3(256), 0, e.st, e.frank,
+                       e.mv_thr, (uint32_t)T.size(), e.N, e.mv_fcls);
+    if ((r = launch_own_rows(e, nullptr, nullptr))) return r;  // the rows carry their peers' failure classes
+  }
+  return hipStreamSynchronize(e.st);  // fk and T are host temporaries
+}
+
 static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   MvArgs a;
-  a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.own = e.own; a.frank = e.frank; a.origin = e.origin;
-  a.nfail = e.nfail; a.mask = e.mask; a.gt = e.mv_gtab + (size_t)g * GT_WORDS;
+  a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.own = e.own; a.fcls = e.mv_fcls; a.fk = e.mv_fk;
+  a.origin = e.origin; a.mask = e.mask; a.gt = e.mv_gtab + (size_t)g * GT_WORDS;
   a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb; a.egress = e.egress; a.err = e.err;
-  a.vis = e.mv_vis; a.lvl = e.lvl; a.tb = e.mv_tb; a.T = e.mv_T; a.area = e.mv_area; a.ctr = e.mv_ctr;
-  a.N = e.N; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
-  a.UB = e.mv.UB; a.BS = e.mv.BS; a.nbins = e.mv.nbins; a.TW = e.mv.TW; a.PW = e.mv.PW; a.ORW = e.ASZP + 4;
+  a.vis = e.mv_vis; a.lvl = e.lvl; a.hlvl = e.mv_hlvl_dev; a.T = e.mv_T; a.area = e.mv_area; a.ctr = e.mv_ctr;
+  a.pool = e.mv_pool; a.pused = e.mv_pused; a.Lt = e.mv_Lt;
+  a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
+  a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
+  a.ORW = e.ASZP + 4;
   a.any_fail = 0;
   for (uint32_t j = 0; j < gr.sg; ++j) a.any_fail |= e.h_nfail_any[gr.s0 + j] ? 1u : 0u;
   a.gcap = e.mv.gcap;
   a.PAIRS = e.PAIRS; a.area_cap = e.mv.area_cap; a.rows_cap = e.mv.rows_cap; a.q_cap = e.mv.q_cap;
+  a.pcap = e.mv.pcap;
   return a;
 }
 
 hipError_t launch_bfs_multi(Engine& e, bool /*record*/) {
-  hipError_t r;
-  const size_t lds_x = mv_hist_bytes(e.mv.nbins) + (size_t)e.mv.PW * e.ASZP * 8;
-  const size_t lds_a = mv_apply_lds_bytes(e.mv.BS);
-  const size_t lds_g = 160 * 1024;
+  hipError_t r = hipSuccess;
+  const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)MV_XT * e.ASZP * 8;
+  const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
+  const size_t lds_g = MV_GLDS;
   if (!e.mv_attr_set) {
     GS_ASZP_DISPATCH(e.ASZP, {
-      if (e.mv.XPT == 2)
-        r = hipFuncSetAttribute((const void*)k_mv_expand<A, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
-      else
-        r = hipFuncSetAttribute((const void*)k_mv_expand<A, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
+      r = hipFuncSetAttribute((const void*)k_mv_expand<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
     });
     if (r != hipSuccess) return r;
     if ((r = hipFuncSetAttribute((const void*)k_mv_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a)))
       return r;
     if ((r = hipFuncSetAttribute((const void*)k_mv_gather, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
       return r;
+    GS_ASZP_DISPATCH(e.ASZP, {
+      r = hipFuncSetAttribute((const void*)k_mv_small<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(e.mv.nbf * 4));
+    });
+    if (r != hipSuccess) return r;
     for (int i = 0; i < 4; ++i)
       if ((r = hipEventCreateWithFlags(&e.mv_ev[i], hipEventDisableTiming)) != hipSuccess) return r;
     e.mv_attr_set = true;
   }
-  const uint32_t bgrid = ((e.mv.nbins + 7) / 8) * 8;
-  const uint32_t xgrid = 512;
-  volatile uint32_t* poll = e.h_err + 8;  // pinned
+  const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8;
+  const uint32_t ggrid = ((e.mv.nbf + 7) / 8) * 8;
+  const uint32_t xgrid = 2048;
+  volatile uint32_t* hl = e.mv_hlvl;  // host-mapped: expand(d) writes lvl[d]
+  volatile uint32_t* hs = e.mv_hlvl + 256;  // host-mapped: the small-level kernel's (level, entries)
+  const size_t lds_s = (size_t)e.mv.nbf * 4;
   for (uint32_t g = 0; g < (uint32_t)e.mv_groups.size(); ++g) {
     const MvGroup& gr = e.mv_groups[g];
     MvArgs a = mv_args(e, gr, g);
-    if ((r = hipMemsetAsync(e.mv_vis, 0, (size_t)e.N * 4, e.st)) != hipSuccess) return r;
-    if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st)) != hipSuccess) return r;
+    if ((r = hipMemsetAsync(e.mv_vis, 0, (size_t)e.N * 4, e.st))) return r;
+    if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st))) return r;
+    if ((r = hipMemsetAsync(e.mv_pused, 0, (size_t)e.mv.nbf * 4, e.st))) return r;
     hipLaunchKernelGGL(k_mv_seed, dim3((gr.nseed + 255) / 256), dim3(256), 0, e.st, a, e.mv_seed + gr.seed0, gr.nseed,
                        e.mv_q[0]);
-    uint32_t nlev = 0;
-    for (uint32_t d = 0; d < 254; ++d) {
-      GS_ASZP_DISPATCH(e.ASZP, {
-        if (e.mv.XPT == 2)
-          hipLaunchKernelGGL((k_mv_expand<A, 2>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, d, e.mv_q[d & 1]);
-        else
-          hipLaunchKernelGGL((k_mv_expand<A, 1>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, d, e.mv_q[d & 1]);
-      });
-      hipLaunchKernelGGL(k_mv_apply, dim3(bgrid), dim3(MV_AT), lds_a, e.st, a, d, e.mv_q[(d + 1) & 1]);
-      // the next frontier's size, polled three levels late so the GPU never idles on the host
-      if ((r = hipMemcpyAsync((void*)(poll + (d & 3)), e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st))) return r;
-      if ((r = hipEventRecord(e.mv_ev[d & 3], e.st))) return r;
-      if (d >= 3) {
-        if ((r = hipEventSynchronize(e.mv_ev[(d - 3) & 3]))) return r;
-        if (poll[(d - 3) & 3] == 0) { nlev = d + 1; break; }
+    uint32_t nlev = 0, d = 0;
+    for (;;) {
+      // small levels in one workgroup, until the frontier is empty or large
+      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, d,
+                                                  e.mv_q[0], e.mv_q[1], e.mv_hstate_dev));
+      if ((r = hipEventRecord(e.mv_ev[0], e.st))) return r;
+      if ((r = hipEventSynchronize(e.mv_ev[0]))) return r;
+      d = hs[0];
+      if (hs[1] == 0) { nlev = d; break; }
+      if (d >= 254) return hipErrorNotSupported;  // frontier still non-empty after 254 levels
+      // large levels: expand + apply; the frontier size of level x is polled two levels late
+      const uint32_t dl = d;
+      bool done = false;
+      for (;; ++d) {
+        if (d >= 254) return hipErrorNotSupported;
+        GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, d,
+                                                    e.mv_q[d & 1]));
+        if ((r = hipEventRecord(e.mv_ev[d & 3], e.st))) return r;
+        hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, d, e.mv_q[(d + 1) & 1]);
+        if (d >= dl + 2) {
+          if ((r = hipEventSynchronize(e.mv_ev[(d - 2) & 3]))) return r;
+          const uint32_t x = hl[d - 2];
+          if (x == 0) { nlev = d + 1; done = true; break; }
+          if (x <= MV_SMALL) { ++d; break; }  // levels d - 1, d are enqueued; small levels from d + 1
+        }
       }
+      if (done) break;
     }
-    if (!nlev) return hipErrorNotSupported;  // frontier still non-empty after 254 levels
-    hipLaunchKernelGGL(k_mv_gather, dim3(bgrid), dim3(MV_GT), lds_g, e.st, a, nlev);
+    hipLaunchKernelGGL(k_mv_gather, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a, nlev);
+    if (e.mv_diag) {  // GS_MV_DIAG=1: entries and records of the group's BFS (diagnostics)
+      std::vector<uint32_t> pu(e.mv.nbf);
+      if ((r = hipMemcpyAsync(pu.data(), e.mv_pused, pu.size() * 4, hipMemcpyDeviceToHost, e.st))) return r;
+      if ((r = hipStreamSynchronize(e.st))) return r;
+      size_t ent = 0, rec = 0, mx = 0;
+      for (uint32_t d = 0; d < nlev; ++d) ent += hl[d];
+      for (uint32_t x : pu) { rec += x; mx = std::max<size_t>(mx, x); }
+      std::fprintf(stderr, "GS_MV_DIAG group %u: levels %u, entries %zu, records %zu (max %zu per fine bin)\n", g,
+                   nlev, ent, rec, mx);
+    }
   }
   return hipGetLastError();
 }

@@ -52,6 +52,7 @@ struct CgArgs {
   uint32_t* prune_acc;
   uint32_t* err;
   uint32_t N, S, ASZ, capin;
+  size_t mso, msu;  // prune-mask strides of (slot, node)
   uint32_t lane_c, lane_l, wave_c;  // register-path bounds (16, 16) and wave-consume bound (64);
                                     // GS_FLAG_NARROW_WAVE_PATH: (4, 4, 8), so small tests reach every path
   size_t PAIRS;
@@ -234,7 +235,7 @@ __device__ inline void apply_prune(const CgArgs& a, uint32_t o, uint32_t ob, uin
     const uint32_t pos = (uint32_t)s >= head ? (uint32_t)s - head : (uint32_t)s + a.ASZ - head;
     hit |= (uint32_t)((uint32_t)s < a.ASZ && pos < L && row[s] == v) << s;
   }
-  if (hit) atomicOr(&a.mask[(size_t)o * a.N + u], hit);
+  if (hit) atomicOr(&a.mask[o * a.mso + u * a.msu], hit);
 }
 
 // ---- prune, register path (len <= 16) ----
@@ -448,6 +449,8 @@ hipError_t launch_consume_prune_g(Engine& e, bool record) {
   a.slot_prunes = e.slot_prunes; a.mask = e.part_on ? e.part_delta : e.mask; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc;
   a.err = e.err;
   a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.capin = e.capin; a.PAIRS = e.PAIRS; a.record = record ? 1 : 0;
+  a.mso = e.part_on ? e.N : e.mso;  // a partition's delta is slot-major
+  a.msu = e.part_on ? 1 : e.msu;
   const bool narrow = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) != 0;
   a.lane_c = narrow ? 4u : 16u;
   a.lane_l = narrow ? 4u : LANE_L;

@@ -78,6 +78,7 @@ static void destroy_engine(Engine* e) {
   if (e->st) hipStreamSynchronize(e->st);
   for (void* p : e->allocs) hipFree(p);
   if (e->h_err) hipHostFree(e->h_err);
+  if (e->mv_hlvl) hipHostFree(e->mv_hlvl);
   for (auto& kv : e->timers)
     for (auto& pr : kv.second.ev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (hipEvent_t x : e->ev_pool) hipEventDestroy(x);
@@ -89,26 +90,38 @@ static void destroy_engine(Engine* e) {
 
 // Sorts (key, id) pairs on the device (stable, so ties stay in id order) and
 // returns the sorted ids in out_ids.
+// Device scratch freed on every exit path.
+struct DevScratch {
+  std::vector<void*> p;
+  template <class T>
+  bool get(T** out, size_t bytes) {
+    void* x = nullptr;
+    if (hipMalloc(&x, bytes ? bytes : 16) != hipSuccess) return false;
+    p.push_back(x);
+    *out = (T*)x;
+    return true;
+  }
+  ~DevScratch() {
+    for (void* x : p) hipFree(x);
+  }
+};
+
 static int sort_ids_by_key(Engine& e, const uint64_t* keys_in, uint32_t* out_ids) {
+  DevScratch sc;
   uint64_t *kin = nullptr, *kout = nullptr;
-  uint32_t *vin = nullptr;
-  hipError_t r;
-  if ((r = hipMalloc(&kin, e.N * 8ull)) != hipSuccess) return fail(GS_ENOMEM, "sort alloc");
-  hipMalloc(&kout, e.N * 8ull);
-  hipMalloc(&vin, e.N * 4ull);
-  if (!kout || !vin) return fail(GS_ENOMEM, "sort alloc");
-  hipMemcpyAsync(kin, keys_in, e.N * 8ull, hipMemcpyDeviceToDevice, e.st);
+  uint32_t* vin = nullptr;
+  void* tmp = nullptr;
+  if (!sc.get(&kin, e.N * 8ull) || !sc.get(&kout, e.N * 8ull) || !sc.get(&vin, e.N * 4ull))
+    return fail(GS_ENOMEM, "sort alloc");
+  HIPC(hipMemcpyAsync(kin, keys_in, e.N * 8ull, hipMemcpyDeviceToDevice, e.st));
   std::vector<uint32_t> ids(e.N);
   for (uint32_t i = 0; i < e.N; ++i) ids[i] = i;
-  hipMemcpyAsync(vin, ids.data(), e.N * 4ull, hipMemcpyHostToDevice, e.st);
+  HIPC(hipMemcpyAsync(vin, ids.data(), e.N * 4ull, hipMemcpyHostToDevice, e.st));
   size_t tmp_bytes = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, out_ids, (int)e.N, 0, 64, e.st);
-  void* tmp = nullptr;
-  hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16);
-  r = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, out_ids, (int)e.N, 0, 64, e.st);
-  hipStreamSynchronize(e.st);
-  hipFree(tmp); hipFree(kin); hipFree(kout); hipFree(vin);
-  if (r != hipSuccess) return fail(GS_EHIP, std::string("radix sort: ") + hipGetErrorString(r));
+  HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, out_ids, (int)e.N, 0, 64, e.st));
+  if (!sc.get(&tmp, tmp_bytes)) return fail(GS_ENOMEM, "sort temp alloc");
+  HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, out_ids, (int)e.N, 0, 64, e.st));
+  HIPC(hipStreamSynchronize(e.st));  // the scratch is freed on return
   return GS_OK;
 }
 
@@ -204,6 +217,12 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
              round_wg_lds_bytes(n, e->fcap, e->ASZP) <= 160 * 1024;
 
   const size_t N = n, S = n_slots, PAIRS = e->PAIRS;
+  e->SP = (uint32_t)((S + 3) & ~(size_t)3);
+  if (mode == GS_BFS_MULTI) {  // node-major masks / egress: a node's slots share one line
+    e->mso = 1; e->msu = e->SP; e->eso = 1; e->esu = e->SP; e->mask_words = N * e->SP;
+  } else {
+    e->mso = N; e->msu = 1; e->eso = N; e->esu = 1; e->mask_words = PAIRS;
+  }
   ALLOC(e->stake, N, 0);
   ALLOC(e->bucket, N, 0);
   ALLOC(e->P, (size_t)NB * (N + 1), 0);
@@ -224,11 +243,11 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   ALLOC(e->slot_prunes, S, 0);
   ALLOC(e->hops, PAIRS, 0xFF);
   ALLOC(e->cnt, PAIRS, 0);
-  ALLOC(e->mask, PAIRS, 0);
+  ALLOC(e->mask, e->mask_words, 0);
   ALLOC(e->inb, (size_t)e->capin * PAIRS, 0);
   ALLOC(e->cmeta, PAIRS, 0);
   ALLOC(e->ckey, (size_t)CACHE_CAP * PAIRS, 0);
-  ALLOC(e->egress, PAIRS, 0);
+  ALLOC(e->egress, std::max(PAIRS, N * e->esu), 0);
   ALLOC(e->prune_round, PAIRS, 0);
   ALLOC(e->egress_acc, PAIRS, 0);
   ALLOC(e->ingress_acc, PAIRS, 0);
@@ -239,7 +258,8 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
     ALLOC(e->q[1], PAIRS, 0);
   }
   if (mode == GS_BFS_BINNED) {  // ~4096 bins of 2^BS consecutive pairs (L2-sized apply working set)
-    ALLOC(e->own, N * (e->ASZP + 4), 0);
+    e->ORW = e->ASZP + 4;
+    ALLOC(e->own, N * e->ORW, 0);
     ALLOC(e->bin_area, PAIRS * e->fcap, 0);
     ALLOC(e->bin_T, e->bin.T_words, 0);
     // pool: one region of 2^BS * capin records per bin (u32 records when narrow)
@@ -250,14 +270,27 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   }
   if (mode == GS_BFS_MULTI) {
     const MvGeom& g = e->mv;
-    ALLOC(e->own, N * (e->ASZP + 4), 0);
+    if (const char* dg = std::getenv("GS_MV_DIAG"); dg && dg[0] == '1') e->mv_diag = true;
+    e->ORW = ((e->ASZP + 1 + e->ASZP / 4) + 3) & ~3u;  // row, meta, the peers' failure classes
+    ALLOC(e->own, N * e->ORW, 0);
     ALLOC(e->mv_vis, N, 0);
     ALLOC(e->mv_q[0], g.q_cap, 0);
     ALLOC(e->mv_q[1], g.q_cap, 0);
-    ALLOC(e->mv_tb, 260, 0);
     ALLOC(e->mv_T, g.rows_cap * g.TW, 0);
     ALLOC(e->mv_area, g.area_cap, 0);
     ALLOC(e->mv_ctr, 4, 0);
+    ALLOC(e->mv_pool, (size_t)g.nbf * g.pcap, 0);
+    ALLOC(e->mv_pused, g.nbf, 0);
+    ALLOC(e->mv_Lt, (size_t)256 * g.nbf, 0);
+    ALLOC(e->mv_fcls, N, 0xFF);
+    ALLOC(e->mv_fk, S, 0);
+    ALLOC(e->mv_thr, S, 0);
+    if (hipHostMalloc(&e->mv_hlvl, 272 * 4, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&e->mv_hlvl_dev, e->mv_hlvl, 0) != hipSuccess) {
+      destroy_engine(e);
+      return fail(GS_ENOMEM, "host-mapped frontier counters");
+    }
+    e->mv_hstate_dev = e->mv_hlvl_dev + 256;
     ALLOC(e->mv_gtab, (size_t)((S + g.GW - 1) / g.GW) * GT_WORDS, 0);
     ALLOC(e->mv_seed, S, 0);
   }
@@ -325,7 +358,7 @@ void gs_destroy(gs_engine* eh) { destroy_engine(reinterpret_cast<Engine*>(eh)); 
   HIPC(hipSetDevice(e->prm.device));
 
 static int reset_pair_state(Engine* e) {
-  HIPC(hipMemsetAsync(e->mask, 0, e->PAIRS * 4, e->st));
+  HIPC(hipMemsetAsync(e->mask, 0, e->mask_words * 4, e->st));
   HIPC(hipMemsetAsync(e->cmeta, 0, e->PAIRS * 4, e->st));
   HIPC(hipMemsetAsync(e->egress_acc, 0, e->PAIRS * 4, e->st));
   HIPC(hipMemsetAsync(e->ingress_acc, 0, e->PAIRS * 4, e->st));
@@ -387,7 +420,7 @@ int gs_init_active_sets(gs_engine* eh) {
   ENGINE(eh);
   if (int s_ = flush_rot_clear(e)) return s_;
   HIPC(launch_init_entries(*e));
-  HIPC(hipMemsetAsync(e->mask, 0, e->PAIRS * 4, e->st));
+  HIPC(hipMemsetAsync(e->mask, 0, e->mask_words * 4, e->st));
   return GS_OK;
 }
 
@@ -434,17 +467,15 @@ int gs_fail_nodes(gs_engine* eh, const double* fraction) {
   ENGINE(eh);
   if (!fraction) return fail(GS_EINVAL, "null fractions");
   if (!e->failed_ranked) {
+    DevScratch sc;
     uint64_t* keys = nullptr;
     uint32_t *ids = nullptr, *sorted = nullptr;
-    HIPC(hipMalloc(&keys, e->N * 8ull));
-    HIPC(hipMalloc(&ids, e->N * 4ull));
-    HIPC(hipMalloc(&sorted, e->N * 4ull));
+    if (!sc.get(&keys, e->N * 8ull) || !sc.get(&ids, e->N * 4ull) || !sc.get(&sorted, e->N * 4ull))
+      return fail(GS_ENOMEM, "fail_nodes scratch");
     HIPC(launch_fail_keys(*e, keys, ids));
-    int s = sort_ids_by_key(*e, keys, sorted);
-    if (s) return s;
+    if (int s = sort_ids_by_key(*e, keys, sorted)) return s;
     HIPC(launch_scatter_rank(*e, sorted, e->frank));
     HIPC(hipStreamSynchronize(e->st));
-    hipFree(keys); hipFree(ids); hipFree(sorted);
     e->failed_ranked = true;
   }
   std::vector<uint32_t> nf(e->S);
@@ -458,6 +489,7 @@ int gs_fail_nodes(gs_engine* eh, const double* fraction) {
     nf[o] = std::max(nf[o], (uint32_t)k);
     e->h_nfail_any[o] = nf[o] ? 1u : 0u;
   }
+  HIPC(mv_update_failures(*e, nf));
   HIPC(hipMemcpyAsync(e->nfail, nf.data(), e->S * 4, hipMemcpyHostToDevice, e->st));
   HIPC(hipStreamSynchronize(e->st));
   return GS_OK;
@@ -692,7 +724,7 @@ int gs_read_pruned(gs_engine* eh, uint32_t slot, uint32_t node, uint32_t* fifo_m
   if (int s = check_err(e)) return s;
   uint32_t m = 0, org = e->slots[slot].origin;
   uint8_t bn = 0, bo = 0;
-  HIPC(hipMemcpyAsync(&m, e->mask + (size_t)slot * e->N + node, 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(&m, e->mask + slot * e->mso + node * e->msu, 4, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpyAsync(&bn, e->bucket + node, 1, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpyAsync(&bo, e->bucket + org, 1, hipMemcpyDeviceToHost, e->st));
   HIPC(hipStreamSynchronize(e->st));
@@ -758,7 +790,11 @@ int gs_read_pruned_all(gs_engine* eh, uint32_t slot, uint32_t* fifo_mask) {
   std::vector<uint32_t> m(N);
   std::vector<uint8_t> b(N);
   std::vector<uint16_t> hl(N * NB);
-  HIPC(hipMemcpyAsync(m.data(), e->mask + slot * N, N * 4, hipMemcpyDeviceToHost, e->st));
+  if (e->msu == 1) {
+    HIPC(hipMemcpyAsync(m.data(), e->mask + slot * e->mso, N * 4, hipMemcpyDeviceToHost, e->st));
+  } else {
+    HIPC(hipMemcpy2DAsync(m.data(), 4, e->mask + slot * e->mso, e->msu * 4, 4, N, hipMemcpyDeviceToHost, e->st));
+  }
   HIPC(hipMemcpyAsync(b.data(), e->bucket, N, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpyAsync(hl.data(), e->hl, N * NB * 2, hipMemcpyDeviceToHost, e->st));
   HIPC(hipStreamSynchronize(e->st));
@@ -780,7 +816,11 @@ int gs_read_counters(gs_engine* eh, uint32_t slot, uint32_t* egress, uint32_t* i
   if (int s = check_err(e)) return s;
   const size_t N = e->N, base = (size_t)slot * N;
   std::vector<uint8_t> eg(N), hp(N), pr(N);
-  HIPC(hipMemcpyAsync(eg.data(), e->egress + base, N, hipMemcpyDeviceToHost, e->st));
+  if (e->esu == 1) {
+    HIPC(hipMemcpyAsync(eg.data(), e->egress + slot * e->eso, N, hipMemcpyDeviceToHost, e->st));
+  } else {
+    HIPC(hipMemcpy2DAsync(eg.data(), 1, e->egress + slot * e->eso, e->esu, 1, N, hipMemcpyDeviceToHost, e->st));
+  }
   HIPC(hipMemcpyAsync(hp.data(), e->hops + base, N, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpyAsync(pr.data(), e->prune_round + base, N, hipMemcpyDeviceToHost, e->st));
   if (ingress) HIPC(hipMemcpyAsync(ingress, e->cnt + base, N * 4, hipMemcpyDeviceToHost, e->st));

@@ -32,8 +32,8 @@ struct BinGeom {
 // records u64 = src | node-in-bin << UB | slot mask << (UB + BS), slot groups of <= GW.
 constexpr uint32_t GT_WORDS = 96;  // per-group table words
 struct MvGeom {
-  uint32_t UB = 0, BS = 0, nbins = 0, GW = 0, XPT = 0, PW = 0, TW = 0, gcap = 0;
-  size_t q_cap = 0, area_cap = 0, rows_cap = 0;
+  uint32_t UB = 0, BSC = 0, BSF = 0, nbc = 0, nbf = 0, GW = 0, TW = 0, gcap = 0;
+  size_t q_cap = 0, area_cap = 0, rows_cap = 0, pcap = 0;
 };
 struct MvGroup { uint32_t s0, sg, seed0, nseed; };
 
@@ -44,6 +44,11 @@ struct Engine {
   uint32_t ASZ = 0, ASZP = 0, fanout = 0, capin = 64;
   uint32_t bfs_mode = GS_BFS_LEVEL;
   uint32_t fcap = 0;             // min(fanout, active_set_size): pushes per node
+  // (slot o, node u) strides of the prune masks and the round's egress bytes: slot-major
+  // (N, 1), or node-major (1, SP) for the multi-source BFS, whose expansion reads every
+  // slot's mask of a node at once (SP = slots rounded up to 4)
+  size_t mso = 0, msu = 1, eso = 0, esu = 1, mask_words = 0;
+  uint32_t SP = 0;
   bool fused = false;            // gs_round runs the one-kernel workgroup round
   bool inb_valid = true;         // inbound records materialized in HBM (step-wise BFS)
   hipStream_t st = nullptr;
@@ -88,7 +93,8 @@ struct Engine {
   uint32_t* lvl = nullptr;  // frontier sizes per level [256]
   // propagation-blocked BFS (GS_BFS_BINNED, gs_bfs_binned.hip)
   BinGeom bin{};
-  uint32_t* own = nullptr;      // [N][ASZP + 4] own-bucket entry rows (word ASZP = hl | bucket << 16)
+  uint32_t* own = nullptr;      // [N][ORW] own-bucket entry rows (word ASZP = hl | bucket << 16; multi: + fcls)
+  uint32_t ORW = 0;
   uint2* bin_area = nullptr;    // expand -> apply records (pair, src), per level, PAIRS * fcap
   uint32_t* bin_T = nullptr;    // [Gmax][nbins + 1] bin starts of each expand workgroup's run
   uint2* bin_pool = nullptr;    // apply -> gather records: one region of 2^BS * capin records per bin
@@ -99,15 +105,24 @@ struct Engine {
   MvGeom mv{};
   uint32_t* mv_vis = nullptr;     // [N] slot masks reached this round (current group)
   uint2* mv_q[2] = {nullptr, nullptr};  // frontier entries (node | entry << 24, slot mask) [q_cap]
-  uint32_t* mv_tb = nullptr;      // [257] first T row of each level
-  uint32_t* mv_T = nullptr;       // [rows_cap][TW] per expand workgroup: run base, bin starts, total
-  unsigned long long* mv_area = nullptr;  // [area_cap] records of the round
+  uint32_t* mv_T = nullptr;       // [rows_cap][TW] per expand workgroup of a level: run base, bin starts, total
+  unsigned long long* mv_area = nullptr;  // [area_cap] records of a level
   uint32_t* mv_ctr = nullptr;     // [4] records used
+  unsigned long long* mv_pool = nullptr;  // [nbf][pcap] records of the round per fine bin
+  uint32_t* mv_pused = nullptr;   // [nbf]
+  uint2* mv_Lt = nullptr;         // [256][nbf] (pool start, count) per level and fine bin
+  uint8_t* mv_fcls = nullptr;     // [N] failure class per node
+  uint8_t* mv_fk = nullptr;       // [S] failure class index per slot
+  uint32_t* mv_thr = nullptr;     // [S] distinct failure counts (scratch)
+  uint32_t* mv_hlvl = nullptr;    // host-mapped [256] frontier sizes (host pointer)
+  uint32_t* mv_hlvl_dev = nullptr;  // its device pointer
+  uint32_t* mv_hstate_dev = nullptr;  // device pointer of mv_hlvl + 256 (small-level kernel's state)
   uint32_t* mv_gtab = nullptr;    // [groups][GT_WORDS]
   uint2* mv_seed = nullptr;       // [S] seed entries (distinct origins) of every group
   std::vector<MvGroup> mv_groups;
   hipEvent_t mv_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool mv_attr_set = false;
+  bool mv_diag = false;  // GS_MV_DIAG=1
   std::vector<uint32_t> h_nfail_any;  // host copy: slot has failed nodes
   // rotation
   uint32_t* rot_list = nullptr;
@@ -183,6 +198,7 @@ bool mv_supported(const MvGeom& g, uint32_t ASZP);
 void mv_build_groups(Engine& e, const std::vector<uint32_t>& origins, const std::vector<uint8_t>& obkt,
                      const std::vector<uint8_t>& bucket, std::vector<uint32_t>& gtab, std::vector<uint2>& seeds);
 hipError_t launch_bfs_multi(Engine& e, bool record);
+hipError_t mv_update_failures(Engine& e, const std::vector<uint32_t>& nf);
 // own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);

@@ -128,17 +128,17 @@ hipError_t launch_scatter_rank(Engine& e, const uint32_t* sorted_ids, uint32_t* 
   return hipGetLastError();
 }
 
-__global__ void k_clear_slot_masks(uint32_t N, uint32_t S, uint32_t node, uint32_t bucket_k,
+__global__ void k_clear_slot_masks(size_t mso, size_t msu, uint32_t S, uint32_t node, uint32_t bucket_k,
                                    const uint8_t* __restrict__ bucket, const uint8_t* __restrict__ obkt,
                                    uint32_t bits, uint32_t* mask) {
   const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= S) return;
   const uint32_t b = min((uint32_t)bucket[node], (uint32_t)obkt[o]);
-  if (b == bucket_k) mask[(size_t)o * N + node] &= ~bits;
+  if (b == bucket_k) mask[o * mso + node * msu] &= ~bits;
 }
 hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket_k, uint32_t bits) {
-  hipLaunchKernelGGL(k_clear_slot_masks, dim3(grid_for(e.S, 256)), dim3(256), 0, e.st, e.N, e.S, node, bucket_k,
-                     e.bucket, e.obkt, bits, e.mask);
+  hipLaunchKernelGGL(k_clear_slot_masks, dim3(grid_for(e.S, 256)), dim3(256), 0, e.st, e.mso, e.msu, e.S, node,
+                     bucket_k, e.bucket, e.obkt, bits, e.mask);
   return hipGetLastError();
 }
 
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void k_rotate_entries(const uint8_t* __restric
 
 // A replaced peer gets a fresh filter: clear its ring slot's prune bit for every
 // slot whose origin uses that entry.
-__global__ void k_rotate_clear(uint32_t N, uint32_t S, const uint8_t* __restrict__ bucket,
+__global__ void k_rotate_clear(size_t mso, size_t msu, uint32_t S, const uint8_t* __restrict__ bucket,
                                const uint8_t* __restrict__ obkt, const uint32_t* __restrict__ rot_list,
                                const uint32_t* __restrict__ rot_count, const uint32_t* __restrict__ rot_changed,
                                uint32_t* __restrict__ mask) {
@@ -243,12 +243,12 @@ __global__ void k_rotate_clear(uint32_t N, uint32_t S, const uint8_t* __restrict
     const uint32_t u = rot_list[i];
     const uint32_t b = min((uint32_t)bucket[u], (uint32_t)obkt[o]);
     const uint32_t m = rot_changed[u * NB + b];
-    if (m) mask[(size_t)o * N + u] &= ~m;
+    if (m) mask[o * mso + u * msu] &= ~m;
   }
 }
 
 hipError_t launch_rotate_clear(Engine& e) {
-  hipLaunchKernelGGL(k_rotate_clear, dim3(grid_for((size_t)e.N * e.S, 256, 2048)), dim3(256), 0, e.st, e.N, e.S,
+  hipLaunchKernelGGL(k_rotate_clear, dim3(grid_for((size_t)e.N * e.S, 256, 2048)), dim3(256), 0, e.st, e.mso, e.msu, e.S,
                      e.bucket, e.obkt, e.rot_list, e.rot_count + e.rot_parity, e.rot_changed, e.mask);
   return hipGetLastError();
 }
@@ -595,6 +595,7 @@ struct CpArgs {
   uint32_t N, S, ASZ, ASZP, capin;
   int record;
   size_t PAIRS;
+  size_t mso, msu;  // prune-mask strides of (slot, node)
 };
 
 
@@ -612,7 +613,7 @@ __device__ inline void apply_prune(const CpArgs& a, uint32_t o, uint32_t ob, uin
     uint32_t slot = head + j;
     if (slot >= a.ASZ) slot -= a.ASZ;
     if (row[slot] == v) {
-      atomicOr(&a.mask[(size_t)o * a.N + u], 1u << slot);
+      atomicOr(&a.mask[o * a.mso + u * a.msu], 1u << slot);
       return;
     }
   }
@@ -876,6 +877,7 @@ hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply,
   a.prune_round = e.prune_round; a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.err = e.err;
   a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc; a.record = record ? 1 : 0;
   a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.ASZP = e.ASZP; a.capin = e.capin; a.PAIRS = e.PAIRS;
+  a.mso = e.mso; a.msu = e.msu;
   const uint32_t grid = grid_for(e.PAIRS, 256, 8192);
   hipError_t r;
   if (prune && (r = hipMemsetAsync(e.slot_prunes, 0, e.S * 4, e.st)) != hipSuccess) return r;
@@ -912,7 +914,8 @@ struct StatsArgs {
   uint32_t* bm;
   gs_round_summary* sum;
   uint32_t N, S, W;
-  uint32_t lo, hi;  // nodes of this pass (a node-range partition passes its own range)
+  uint32_t lo, hi;
+  size_t eso, esu;  // egress strides of (slot, node)  // nodes of this pass (a node-range partition passes its own range)
 };
 
 // FULL: the step-wise gs_record_round (reads the per-round counters of every pair);
@@ -944,7 +947,7 @@ __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
     if (hh != 0xFF) {
       ++vis;
       atomicAdd(&h[hh], 1u);
-      if (FULL || EG) a.egress_acc[p] += a.egress[p];
+      if (FULL || EG) a.egress_acc[p] += a.egress[o * a.eso + v * a.esu];
     } else if (!(nf && a.frank[v] < nf)) {
       a.strand[p] += 1;
       ++sc;
@@ -1063,7 +1066,7 @@ hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   a.hops = e.hops; a.cnt = e.cnt; a.egress = e.egress; a.prune_round = e.prune_round; a.slot_prunes = e.slot_prunes;
   a.egress_acc = e.egress_acc; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc; a.strand = e.strand;
   a.rs_u32 = e.rs_u32; a.rs_ssum = e.rs_ssum; a.rs_hist = e.rs_hist; a.hist_acc = e.hist_acc; a.bm = e.bm;
-  a.sum = e.sum; a.N = e.N; a.S = e.S; a.W = e.bm_words;
+  a.sum = e.sum; a.N = e.N; a.S = e.S; a.W = e.bm_words; a.eso = e.eso; a.esu = e.esu;
   a.lo = e.part_on ? e.part_lo : 0u;
   a.hi = e.part_on ? e.part_hi : e.N;
   uint32_t gx = grid_for(e.N, 256, std::max<uint32_t>(64, 2048 / std::max<uint32_t>(e.S, 1)));

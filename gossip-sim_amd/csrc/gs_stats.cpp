@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -233,7 +234,7 @@ int gs_run_simulations(const gs_sim_config* cfg, const uint64_t* stakes, uint32_
   std::vector<gs_round_summary> sums((size_t)rounds * n_sims + 1);
   size_t nsum = 0;
   CK(gs_read_round_summaries(e, sums.data(), sums.size(), &nsum));
-  auto* res = new gs_sim_result();
+  std::unique_ptr<gs_sim_result> res(new gs_sim_result());  // released to *out only on success
   res->sims.resize(n_sims);
   uint64_t max_stake = 0;
   for (uint32_t v = 0; v < n; ++v) max_stake = std::max(max_stake, stakes[v]);
@@ -354,7 +355,7 @@ int gs_run_simulations(const gs_sim_config* cfg, const uint64_t* stakes, uint32_
   }
 #undef CK
   gs_destroy(e);
-  *out = res;
+  *out = res.release();
   return GS_OK;
 }
 

@@ -36,6 +36,31 @@ def shard(n_units, rank, world):
     return list(range(rank, n_units, world))
 
 
+def shard_range(n_units, rank, world):
+    """Contiguous units [lo, hi) owned by `rank` (origin sharding of one network)."""
+    return n_units * rank // world, n_units * (rank + 1) // world
+
+
+def gather_rows(dist, local, n_units, world, *, row_bytes, group=None):
+    """local: [rows, n_local * row_bytes] uint8 of this rank's contiguous units
+    (shard_range). Returns [rows, n_units * row_bytes] with every rank's columns,
+    assembled by one all-reduce(SUM) of a zero-padded int64 buffer (exact: each byte
+    has one owner). On the "nccl" backend (RCCL over xGMI) the buffer lives on the
+    rank's current GPU."""
+    torch, tdist = dist
+    rank = tdist.get_rank(group)
+    lo, hi = shard_range(n_units, rank, world)
+    rows = local.shape[0]
+    full = np.zeros((rows, n_units * row_bytes), dtype=np.uint8)
+    full[:, lo * row_bytes:hi * row_bytes] = local
+    assert (n_units * row_bytes) % 8 == 0
+    t = torch.from_numpy(full.view(np.int64).copy())
+    if tdist.get_backend(group) == "nccl":
+        t = t.to(f"cuda:{torch.cuda.current_device()}")
+    tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=group)
+    return t.cpu().numpy().view(np.uint8).reshape(rows, -1)
+
+
 def _dist_info(group):
     try:
         import torch.distributed as tdist
