@@ -171,7 +171,10 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
     summ = eng.summaries()
     E = float(summ["pushes"].astype("float64").sum())
     V = float(summ["visited"].astype("float64").sum())
-    fam = {k: eng.kernel_time(k)[0] for k in ("bfs", "consume", "rotate", "stats")}
+    fam = {k: eng.kernel_time(k)[0] for k in ("bfs", "gather", "gather_consume", "consume", "rotate", "stats")}
+    for k in ("gather", "gather_consume"):
+        if not fam[k]:
+            del fam[k]
     info = eng.info()
     eng.close()
     mode = {2: "level", 3: "binned", 4: "multi"}.get(info["bfs_mode"], str(info["bfs_mode"]))
@@ -182,7 +185,11 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
             "edges_per_s": E / dt, "origin_rounds_per_s": S * steps / dt,
             "pushes_per_origin_round": E / (S * steps),
             "us_per_round": {k: round(v * 1e3 / steps, 1) for k, v in fam.items()},
-            "bfs_roofline": roofline(bp, fam["bfs"], steps, f"BFS ({mode}: expand/apply per level + gather)",
+            # multi: the gather that writes hops / in-degrees runs fused with consume; its whole
+            # time is charged to the BFS (conservative: the consume work inside it is counted too)
+            "bfs_roofline": roofline(bp, fam["bfs"] + fam.get("gather", 0.0) + fam.get("gather_consume", 0.0), steps,
+                                     f"BFS ({mode}: " + ("expand/apply per level + fused gather/consume)" if mode == "multi"
+                                                         else "per level)"),
                                      "B_prop (SURVEY 8d), summed over slots", f"bfs_{mode}_c4")}
 
 
@@ -219,7 +226,7 @@ def c3_leg(gs, synth, args, nodes=100_000, warmup=5, steps=20):
         Ve = float(s["visited"].astype("float64").sum())
         E += Ee
         bp += b_prop(Ve, Ee, asz)
-        b_ms += e.kernel_time("bfs")[0]
+        b_ms += sum(e.kernel_time(k)[0] for k in ("bfs", "gather", "gather_consume"))
         mode = {2: "level", 3: "binned", 4: "multi"}.get(e.info()["bfs_mode"])
         e.close()
     return {"workload": f"C3 per-GPU share: {nodes}-node network, active-set-size sweep values 12 and 20, one "
@@ -251,6 +258,7 @@ def main():
     ap.add_argument("--split-round", action="store_true", help="step kernels instead of the one-kernel round")
     ap.add_argument("--no-large", action="store_true", help="skip the c4 / c3 legs")
     ap.add_argument("--only-large", action="store_true", help="run only the c4 / c3 legs (A/B of BFS modes)")
+    ap.add_argument("--legs", default="c4,c3", help="with --only-large: which legs (e.g. c4 for a PMC pass)")
     ap.add_argument("--shard-origins", action="store_true",
                     help="ranks split the origins of ONE network (strong scaling) instead of one network each")
     ap.add_argument("--check-shard", action="store_true",
@@ -262,7 +270,8 @@ def main():
     import gossip_sim_amd.synth as synth
 
     if args.only_large:
-        out = {"c4": c4_leg(gs, synth, args), "c3": c3_leg(gs, synth, args)}
+        legs = {"c4": c4_leg, "c3": c3_leg}
+        out = {k: legs[k](gs, synth, args) for k in args.legs.split(",")}
         print(json.dumps(out), flush=True)
         return
 

@@ -36,6 +36,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "gs_consume_dev.h"
 #include "gs_device.h"
 #include "gs_internal.h"
 
@@ -74,7 +75,12 @@ struct MvArgs {
   unsigned long long* pool;  // [nbf][pcap] records of the round, per fine bin, level runs
   uint32_t* pused;        // [nbf] records in each fine bin's pool region
   uint2* Lt;              // [256][nbf] (pool start, count) of fine bin f at level d
-  uint32_t N, SP, ASZ, fanout, capin, s0, Sg, UB, BSC, BSF, nbc, nbf, TW, ORW, any_fail, gcap;
+  uint32_t* cmeta;        // fused consume (gs_round): the received caches, as in gs_consume_g.hip
+  uint32_t* ckey;
+  uint8_t* prune_round;
+  uint32_t* ingress_acc;
+  uint32_t N, SP, ASZ, fanout, capin, s0, Sg, UB, BSC, BSF, nbc, nbf, TW, ORW, any_fail, gcap, gcap_c;
+  uint32_t lane_c, wave_c, record;
   size_t PAIRS, area_cap, rows_cap, q_cap, pcap;
 };
 
@@ -500,42 +506,40 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2
 // --------------------------------------------------------------- gather ----
 constexpr uint32_t MV_GC = 12;        // records per gather thread kept in registers between the passes
 constexpr uint32_t MV_GLDS = 78 * 1024;  // gather LDS: two workgroups per CU
+constexpr uint32_t MV_WSCR = 64 + CACHE_CAP;  // fused consume: per-wave LDS scratch (u32)
+constexpr uint32_t MV_CSCR = (MV_GT / 64) * MV_WSCR * 4;  // bytes of all waves' scratch
 
 __host__ __device__ inline size_t mv_gather_fixed_bytes(uint32_t BSF) {
   return 4 * (256 + 257 + 2 * (((size_t)1 << BSF) + 1) + 16 + 32);
 }
 
-// After the last level, per fine bin: the bin's records of every level (its pool runs, in
-// level order) as an LDS CSR by destination, then per (slot, node) the in-degree, the
-// inbound rows and the hop, coalesced over nodes.
-__global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t f = mv_xcd_bin(blockIdx.x, a.nbf);
-  if (f >= a.nbf) return;
-  const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BSF = a.BSF, BP = 1u << BSF, BPm = BP - 1, Sg = a.Sg;
-  const uint32_t v0 = f << BSF;
-  if (v0 >= a.N) return;
-  const uint32_t nv = min(BP, a.N - v0);
+// The LDS CSR of one fine bin's records: cn[i] .. cn[i + 1] (minus the range base) index
+// node i's records keys[] = hop << 24 | src and msk[] = slot masks.
+struct MvCsr {
+  uint32_t *rs, *rp, *cn, *cur, *ctl, *sorg, *keys, *msk;
+};
+
+// After the last level, per fine bin f: the bin's records of every level (its pool runs,
+// in level order) as an LDS CSR by destination. Nodes whose records exceed gcap are
+// taken in consecutive ranges; body(lo, hi, base) runs on each range (all threads; no
+// barrier inside body is needed, one follows it).
+template <class Body>
+__device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, uint32_t nv, uint32_t gcap,
+                                  const MvCsr& L, Body body) {
+  const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BSF = a.BSF, BP = 1u << BSF, BPm = BP - 1;
   const uint32_t um = (1u << UB) - 1;
-  uint32_t* rs = reinterpret_cast<uint32_t*>(smem);  // [256] pool start of level d's run
-  uint32_t* rp = rs + 256;                           // [257] records before level d's run
-  uint32_t* cn = rp + 257;                           // [BP + 1] records per node -> CSR starts
-  uint32_t* cur = cn + BP + 1;                       // [BP + 1] placement cursors
-  uint32_t* ctl = cur + BP + 1;                      // [16]
-  uint32_t* sorg = ctl + 16;                         // [32]
-  uint32_t* keys = sorg + 32;                        // [gcap] hop << 24 | src
-  uint32_t* msk = keys + a.gcap;                     // [gcap] slot masks
+  uint32_t *rs = L.rs, *rp = L.rp, *cn = L.cn, *cur = L.cur, *ctl = L.ctl, *keys = L.keys, *msk = L.msk;
   const unsigned long long* pool = a.pool + (size_t)f * a.pcap;
   for (uint32_t i = tid; i <= BP; i += MV_GT) cn[i] = 0;
-  if (tid < Sg) sorg[tid] = a.origin[a.s0 + tid];
+  if (tid < a.Sg) L.sorg[tid] = a.origin[a.s0 + tid];
   {  // the run table: thread d reads level d's (start, count); exclusive prefix of the counts
     uint32_t n = 0;
     if (tid < 256) {
       rs[tid] = 0;
       if (tid < nlev && a.lvl[tid]) {  // an empty level wrote no run
-        const uint2 L = a.Lt[(size_t)tid * a.nbf + f];
-        rs[tid] = L.x;
-        n = L.y;
+        const uint2 R = a.Lt[(size_t)tid * a.nbf + f];
+        rs[tid] = R.x;
+        n = R.y;
       }
     }
     const uint32_t incl = wave_incl_scan(n);
@@ -574,62 +578,235 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
   const uint32_t E2 = mv_block_scan(cn, BP, ctl);
   if (tid == 0) cn[BP] = E2;
   __syncthreads();
-  // 2. node ranges whose records fit the LDS CSR (one range unless the bin is heavy)
-  bool over = false;
-  for (uint32_t lo = 0; lo < nv;) {
+  // 2. node ranges whose records fit the LDS CSR (one range unless the bin is heavy); the
+  // register-held records are placed in the first range only (they are dead afterwards:
+  // later ranges re-read the pool), so they do not stay live across body
+  auto range = [&](uint32_t lo) {
     if (tid == 0) {
       uint32_t h = lo;
-      while (h < nv && cn[h + 1] - cn[lo] <= a.gcap) ++h;
+      while (h < nv && cn[h + 1] - cn[lo] <= gcap) ++h;
       if (h == lo) { atomicOr(a.err, ERR_MV_CAP); h = nv; }  // one node beyond the LDS CSR
       ctl[15] = h;
     }
     __syncthreads();
     const uint32_t hi = ctl[15];
-    const uint32_t base = cn[lo];
-    for (uint32_t i = lo + tid; i < hi; i += MV_GT) cur[i] = cn[i] - base;
+    for (uint32_t i = lo + tid; i < hi; i += MV_GT) cur[i] = cn[i] - cn[lo];
     __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < MV_GC; ++j) {
-      const uint32_t vl = vc[j];
-      if (vl == 0xFFFFFFFFu || vl < lo || vl >= hi) continue;
-      const uint32_t p = atomicAdd(&cur[vl], 1u);
-      if (p < a.gcap) { keys[p] = kc[j]; msk[p] = mc[j]; }
-    }
-    lv = 0;
-    for (uint32_t t = tid + MV_GC * MV_GT; t < Etot; t += MV_GT) {
-      while (t >= rp[lv + 1]) ++lv;
-      const unsigned long long rec = pool[rs[lv] + (t - rp[lv])];
+    return hi;
+  };
+  auto place_pool = [&](uint32_t lo, uint32_t hi, uint32_t t0) {
+    uint32_t lp = 0;
+    for (uint32_t t = tid + t0; t < Etot; t += MV_GT) {
+      while (t >= rp[lp + 1]) ++lp;
+      const unsigned long long rec = pool[rs[lp] + (t - rp[lp])];
       const uint32_t vl = (uint32_t)(rec >> UB) & BPm;
       if (vl < lo || vl >= hi) continue;
       const uint32_t p = atomicAdd(&cur[vl], 1u);
-      if (p < a.gcap) {
-        keys[p] = ((lv + 1) << 24) | ((uint32_t)rec & um);
+      if (p < gcap) {
+        keys[p] = ((lp + 1) << 24) | ((uint32_t)rec & um);
         msk[p] = (uint32_t)(rec >> (UB + BSC));
       }
     }
     __syncthreads();
-    // 3. per (slot, node): in-degree, inbound rows, hop; coalesced over nodes
+  };
+  uint32_t hi = range(0);
+#pragma unroll
+  for (uint32_t j = 0; j < MV_GC; ++j) {
+    const uint32_t vl = vc[j];
+    if (vl >= hi) continue;  // (also the empty marker)
+    const uint32_t p = atomicAdd(&cur[vl], 1u);
+    if (p < gcap) { keys[p] = kc[j]; msk[p] = mc[j]; }
+  }
+  place_pool(0, hi, MV_GC * MV_GT);
+  body(0u, hi, 0u);
+  __syncthreads();
+  for (uint32_t lo = hi; lo < nv; lo = hi) {
+    hi = range(lo);
+    place_pool(lo, hi, 0);
+    body(lo, hi, cn[lo]);
+    __syncthreads();
+  }
+}
+
+__device__ inline MvCsr mv_csr_lds(unsigned char* smem, uint32_t BP, uint32_t gcap) {
+  MvCsr L;
+  L.rs = reinterpret_cast<uint32_t*>(smem);  // [256] pool start of level d's run
+  L.rp = L.rs + 256;                         // [257] records before level d's run
+  L.cn = L.rp + 257;                         // [BP + 1] records per node -> CSR starts
+  L.cur = L.cn + BP + 1;                     // [BP + 1] placement cursors
+  L.ctl = L.cur + BP + 1;                    // [16]
+  L.sorg = L.ctl + 16;                       // [32]
+  L.keys = L.sorg + 32;                      // [gcap] hop << 24 | src
+  L.msk = L.keys + gcap;                     // [gcap] slot masks
+  return L;
+}
+
+// Per (slot, node) of the fine bin: in-degree, the inbound rows and the hop, coalesced
+// over nodes (the step API's gs_run_gossip; gs_round fuses this with consume below).
+__global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t f = mv_xcd_bin(blockIdx.x, a.nbf);
+  if (f >= a.nbf) return;
+  const uint32_t tid = threadIdx.x, BP = 1u << a.BSF, Sg = a.Sg, v0 = f << a.BSF;
+  if (v0 >= a.N) return;
+  const uint32_t nv = min(BP, a.N - v0), gcap = a.gcap;
+  const MvCsr L = mv_csr_lds(smem, BP, gcap);
+  bool over = false;
+  mv_bin_csr(a, f, nlev, nv, gcap, L, [&](uint32_t lo, uint32_t hi, uint32_t base) {
     for (uint32_t i = lo + tid; i < hi; i += MV_GT) {
-      const uint32_t v = v0 + i, r0 = cn[i] - base, r1 = min(cn[i + 1] - base, a.gcap);
+      const uint32_t v = v0 + i, r0 = L.cn[i] - base, r1 = min(L.cn[i + 1] - base, gcap);
       for (uint32_t j = 0; j < Sg; ++j) {
         const size_t p = (size_t)(a.s0 + j) * a.N + v;
         uint32_t cc = 0, mh = 0xFFu;
-        for (uint32_t r = r0;; ++r, ++cc) {  // trip cc writes row cc: lanes store the same row together
-          while (r < r1 && !((msk[r] >> j) & 1u)) ++r;
-          if (r >= r1) break;
-          const uint32_t key = keys[r];
+        for (uint32_t r = r0; r < r1; ++r) {
+          if (!((L.msk[r] >> j) & 1u)) continue;
+          const uint32_t key = L.keys[r];
           if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = key;
           mh = min(mh, key >> 24);
+          ++cc;
         }
         over |= cc > a.capin;
         a.cnt[p] = cc;
-        a.hops[p] = (uint8_t)(v == sorg[j] ? 0u : (cc ? mh : 0xFFu));
+        a.hops[p] = (uint8_t)(v == L.sorg[j] ? 0u : (cc ? mh : 0xFFu));
       }
     }
-    __syncthreads();
-    lo = hi;
-  }
+  });
   if (over) atomicOr(a.err, ERR_INBOUND);
+}
+
+// After a pair's consume: in-degree recorded, a due prune queued (k_cg_prune finds it by
+// its meta word), else the previous round's pruned-len and prune count cleared.
+__device__ inline void mv_after_consume(const MvArgs& a, uint32_t q, uint32_t meta, uint32_t c, uint32_t len,
+                                        uint32_t up) {
+  const bool due = up >= MIN_NUM_UPSERTS;
+  const uint32_t nm = due ? (len | (up << 8) | (meta & 0xFF0000u)) : (len | (up << 8));
+  if (nm != meta) a.cmeta[q] = nm;
+  if (!due) a.prune_round[q] = 0;
+  if (a.record && c) a.ingress_acc[q] += c;
+}
+
+// gs_round's gather + consume_messages (gossip.rs:601-607, 618-653): per (slot, node)
+// of the fine bin, the pair's records are filtered from the node's LDS list straight
+// into registers (the inbound rows are never written), then the received-cache update
+// of gs_consume_dev.h; in-degree and hop as in k_mv_gather. Lanes walk nodes, so the
+// cache rows stay coalesced. Pairs with in-degree > lane_c are taken by the whole wave
+// (records compacted by ballot, sorted across lanes), > wave_c by one lane.
+__global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void k_mv_consume(MvArgs a, uint32_t nlev) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t f = mv_xcd_bin(blockIdx.x, a.nbf);
+  if (f >= a.nbf) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, BP = 1u << a.BSF, Sg = a.Sg, v0 = f << a.BSF;
+  if (v0 >= a.N) return;
+  const uint32_t nv = min(BP, a.N - v0), gcap = a.gcap_c;
+  uint32_t* wscr = reinterpret_cast<uint32_t*>(smem) + (tid >> 6) * MV_WSCR;  // [64] keys, [CACHE_CAP] cache
+  const MvCsr L = mv_csr_lds(smem + MV_CSCR, BP, gcap);
+  const size_t PAIRS = a.PAIRS;
+  uint32_t over = 0, errf = 0;
+  mv_bin_csr(a, f, nlev, nv, gcap, L, [&](uint32_t lo, uint32_t hi, uint32_t base) {
+    for (uint32_t i0 = lo; i0 < hi; i0 += MV_GT) {  // block-uniform trip count
+      const uint32_t i = i0 + tid;
+      const bool in = i < hi;
+      const uint32_t v = v0 + i;
+      const uint32_t r0 = in ? L.cn[i] - base : 0u, r1 = in ? min(L.cn[i + 1] - base, gcap) : 0u;
+      for (uint32_t j = 0; j < Sg; ++j) {
+        const uint32_t q = (a.s0 + j) * a.N + v;
+        // the slot's records of the node: a list of <= 64 records is filtered to a bitmap
+        // (one bit per record), then its first 16 matches are extracted; a longer list
+        // collects them record by record
+        uint32_t rk[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) rk[t] = 0xFFFFFFFFu;
+        const uint32_t Ln = r1 - r0;
+        uint32_t c = 0, mh = 0xFFu, blo = 0, bhi = 0;
+        if (Ln <= 64) {
+          const uint32_t l1 = min(Ln, 32u);
+          for (uint32_t k = 0; k < l1; ++k) blo |= ((L.msk[r0 + k] >> j) & 1u) << k;
+          for (uint32_t k = 32; k < Ln; ++k) bhi |= ((L.msk[r0 + k] >> j) & 1u) << (k - 32);
+          c = (uint32_t)(__popc(blo) + __popc(bhi));
+        } else {
+          for (uint32_t r = r0; r < r1; ++r) {
+            if (!((L.msk[r] >> j) & 1u)) continue;
+            const uint32_t key = L.keys[r];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) rk[t] = c == (uint32_t)t ? key : rk[t];
+            ++c;
+          }
+        }
+        const uint32_t wx = active_max<5>(min(c, 16u));
+#pragma unroll
+        for (uint32_t t = 0; t < 16; ++t) {
+          if (t >= wx) break;
+          if (blo | bhi) {
+            const uint32_t pos = blo ? (uint32_t)__builtin_ctz(blo) : 32u + (uint32_t)__builtin_ctz(bhi);
+            if (blo) blo &= blo - 1; else bhi &= bhi - 1;
+            rk[t] = L.keys[r0 + pos];
+          }
+          mh = min(mh, rk[t] >> 24);
+        }
+        if (c > 16) {  // (rare) the hop over every match
+          mh = 0xFFu;
+          for (uint32_t r = r0; r < r1; ++r)
+            if ((L.msk[r] >> j) & 1u) mh = min(mh, L.keys[r] >> 24);
+        }
+        uint32_t meta = 0;
+        if (in) {
+          a.cnt[q] = c;
+          a.hops[q] = (uint8_t)(v == L.sorg[j] ? 0u : (c ? mh : 0xFFu));
+          meta = ntl(&a.cmeta[q]);
+          if (c > a.capin) { over = 1; c = a.capin; }
+        }
+        uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
+        const bool heavy = in && c > a.lane_c;
+        if (in && !heavy) {
+          if (c) {
+            const uint32_t wc = active_max<5>(c);
+            sort_ranked(rk, wc);
+            cache_update_lane(a.ckey, PAIRS, q, rk, c, wc, len, up, errf);
+          }
+          mv_after_consume(a, q, meta, c, len, up);
+        }
+        uint64_t hv = __ballot(heavy);
+        while (hv) {  // the wave's heavy pairs, one at a time
+          const int hl = __ffsll((long long)hv) - 1;
+          hv &= hv - 1;
+          const uint32_t hq = (uint32_t)__shfl((int)q, hl);
+          const uint32_t hmeta = (uint32_t)__shfl((int)meta, hl);
+          const uint32_t hc = (uint32_t)__shfl((int)c, hl);
+          const uint32_t h0 = (uint32_t)__shfl((int)r0, hl), h1 = (uint32_t)__shfl((int)r1, hl);
+          uint32_t hlen = hmeta & 0xFF, hup = (hmeta >> 8) & 0xFF;
+          if (hc <= a.wave_c) {
+            uint32_t nb = 0;  // compact the pair's records into wscr[0..hc), then sort across lanes
+            for (uint32_t rb = h0; rb < h1; rb += 64) {
+              const uint32_t r = rb + lane;
+              const bool m = r < h1 && ((L.msk[r] >> j) & 1u);
+              const uint64_t bm = __ballot(m);
+              const uint32_t pos = nb + (uint32_t)__popcll(bm & ((1ull << lane) - 1));
+              if (m && pos < 64) wscr[pos] = L.keys[r];
+              nb += (uint32_t)__popcll(bm);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t key = wave_sort(lane < hc ? wscr[lane] : 0xFFFFFFFFu);
+            __builtin_amdgcn_wave_barrier();
+            cache_update_wave(a.ckey, PAIRS, hq, key, hc, hlen, hup, wscr + 64, errf);
+          } else {
+            cache_update_serial(a.ckey, PAIRS, hq, hc, hlen, hup, errf, [&](uint32_t k, uint32_t prev) {
+              uint32_t best = 0xFFFFFFFFu;
+              for (uint32_t r = h0; r < h1; ++r) {
+                if (!((L.msk[r] >> j) & 1u)) continue;
+                const uint32_t x = L.keys[r];
+                if ((k == 0 || x > prev) && x < best) best = x;
+              }
+              return best;
+            });
+          }
+          if (lane == 0) mv_after_consume(a, hq, hmeta, hc, hlen, hup);
+        }
+      }
+    }
+  });
+  if (over) atomicOr(a.err, ERR_INBOUND);
+  if (errf) atomicOr(a.err, errf);
 }
 
 __global__ void k_mv_seed(MvArgs a, const uint2* __restrict__ seeds, uint32_t nseed, uint2* __restrict__ q0) {
@@ -685,6 +862,7 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   const size_t rpn = (size_t)ASZ * std::min<size_t>(sg, 4) + 16;  // pool records per node (average over a bin)
   g.pcap = ((size_t)1 << g.BSF) * rpn;
   g.gcap = (uint32_t)((MV_GLDS - mv_gather_fixed_bytes(g.BSF)) / 8);
+  g.gcap_c = (uint32_t)((MV_GLDS - MV_CSCR - mv_gather_fixed_bytes(g.BSF)) / 8);
 }
 
 bool mv_supported(const MvGeom& g, uint32_t ASZP) {
@@ -762,16 +940,22 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.pool = e.mv_pool; a.pused = e.mv_pused; a.Lt = e.mv_Lt;
   a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
-  a.ORW = e.ASZP + 4;
+  a.ORW = e.ORW;
   a.any_fail = 0;
   for (uint32_t j = 0; j < gr.sg; ++j) a.any_fail |= e.h_nfail_any[gr.s0 + j] ? 1u : 0u;
   a.gcap = e.mv.gcap;
+  a.gcap_c = e.mv.gcap_c;
+  a.cmeta = e.cmeta; a.ckey = e.ckey; a.prune_round = e.prune_round; a.ingress_acc = e.ingress_acc;
+  const bool narrow = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) != 0;  // small tests reach every consume path
+  a.lane_c = narrow ? 4u : 16u;
+  a.wave_c = narrow ? 8u : 64u;
+  a.record = 0;
   a.PAIRS = e.PAIRS; a.area_cap = e.mv.area_cap; a.rows_cap = e.mv.rows_cap; a.q_cap = e.mv.q_cap;
   a.pcap = e.mv.pcap;
   return a;
 }
 
-hipError_t launch_bfs_multi(Engine& e, bool /*record*/) {
+hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
   hipError_t r = hipSuccess;
   const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)MV_XT * e.ASZP * 8;
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
@@ -784,6 +968,8 @@ hipError_t launch_bfs_multi(Engine& e, bool /*record*/) {
     if ((r = hipFuncSetAttribute((const void*)k_mv_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a)))
       return r;
     if ((r = hipFuncSetAttribute((const void*)k_mv_gather, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
+      return r;
+    if ((r = hipFuncSetAttribute((const void*)k_mv_consume, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
       return r;
     GS_ASZP_DISPATCH(e.ASZP, {
       r = hipFuncSetAttribute((const void*)k_mv_small<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -803,6 +989,9 @@ hipError_t launch_bfs_multi(Engine& e, bool /*record*/) {
   for (uint32_t g = 0; g < (uint32_t)e.mv_groups.size(); ++g) {
     const MvGroup& gr = e.mv_groups[g];
     MvArgs a = mv_args(e, gr, g);
+    a.record = record ? 1u : 0u;
+    hipEvent_t t0;
+    e.tbegin("bfs", &t0);
     if ((r = hipMemsetAsync(e.mv_vis, 0, (size_t)e.N * 4, e.st))) return r;
     if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st))) return r;
     if ((r = hipMemsetAsync(e.mv_pused, 0, (size_t)e.mv.nbf * 4, e.st))) return r;
@@ -836,7 +1025,11 @@ hipError_t launch_bfs_multi(Engine& e, bool /*record*/) {
       }
       if (done) break;
     }
-    hipLaunchKernelGGL(k_mv_gather, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a, nlev);
+    e.tend("bfs", t0);
+    e.tbegin(consume ? "gather_consume" : "gather", &t0);
+    if (consume) hipLaunchKernelGGL(k_mv_consume, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a, nlev);
+    else hipLaunchKernelGGL(k_mv_gather, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a, nlev);
+    e.tend(consume ? "gather_consume" : "gather", t0);
     if (e.mv_diag) {  // GS_MV_DIAG=1: entries and records of the group's BFS (diagnostics)
       std::vector<uint32_t> pu(e.mv.nbf);
       if ((r = hipMemcpyAsync(pu.data(), e.mv_pused, pu.size() * 4, hipMemcpyDeviceToHost, e.st))) return r;

@@ -17,6 +17,7 @@
 // gs_send_prunes / gs_prune_connections.
 #include <algorithm>
 
+#include "gs_consume_dev.h"
 #include "gs_device.h"
 #include "gs_internal.h"
 
@@ -59,17 +60,6 @@ struct CgArgs {
   int record;
 };
 
-template <class T>
-__device__ inline T ntl(const T* p) { return __builtin_nontemporal_load(p); }
-
-template <int NC>
-__device__ inline uint32_t match24(const uint32_t (&rk)[16], uint32_t k) {
-  uint32_t m = 0;
-#pragma unroll
-  for (int j = 0; j < NC; ++j) m |= (uint32_t)((rk[j] & CK_ID) == k) << j;
-  return m;
-}
-
 // ---- consume, register path (1 <= c <= 16) ----
 __device__ inline void consume_lane(const CgArgs& a, uint32_t q, uint32_t c, uint32_t& len, uint32_t& up,
                                     uint32_t& errf) {
@@ -81,133 +71,30 @@ __device__ inline void consume_lane(const CgArgs& a, uint32_t q, uint32_t c, uin
   asm volatile("" ::: "memory");
 #pragma unroll
   for (int j = 0; j < 16; ++j) rk[j] = (uint32_t)j < c ? rk[j] : 0xFFFFFFFFu;
-  if (wc <= 4) sort_net<4>(rk);
-  else if (wc <= 8) sort_net<8>(rk);
-  else sort_net<16>(rk);
-  uint32_t present = 0, w0 = 0, w1 = 0;
-  int idx0 = -1, idx1 = -1;
-  const uint32_t wl = active_max<7>(len);
-  for (uint32_t i0 = 0; i0 < wl; i0 += 8) {
-    uint32_t kc[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) kc[t] = i0 + t < wl ? ntl(&(a.ckey + (size_t)(i0 + t) * PAIRS)[q]) : 0u;
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const uint32_t i = i0 + t;
-      const uint32_t k = i < len ? ck_id(kc[t]) : 0xFFFFFFFFu;
-      const uint32_t m = wc <= 4 ? match24<4>(rk, k) : wc <= 8 ? match24<8>(rk, k) : match24<16>(rk, k);
-      present |= m;
-      if (m & 1u) { idx0 = (int)i; w0 = kc[t]; }
-      if (m & 2u) { idx1 = (int)i; w1 = kc[t]; }
-    }
-  }
-  up = up < 255 ? up + 1 : 255;  // rank 0 (received_cache.rs:84-86)
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {  // timely: score += 1, inserted regardless of the 50-key cap
-    if ((uint32_t)j >= c) break;
-    const int idx = j == 0 ? idx0 : idx1;
-    if (idx >= 0) {
-      (a.ckey + (size_t)idx * PAIRS)[q] = ck_bump(j == 0 ? w0 : w1);
-    } else if (len < CACHE_CAP) {
-      (a.ckey + (size_t)len * PAIRS)[q] = ck_make(rk[j] & CK_ID, 1u);
-      ++len;
-    } else {
-      errf |= ERR_CACHE;
-    }
-  }
-#pragma unroll
-  for (int j = 2; j < 16; ++j)  // rank order; inserted only while len < 50 (received_cache.rs:91-97)
-    if ((uint32_t)j < c && !((present >> j) & 1u) && len < CACHE_LIMIT) {
-      (a.ckey + (size_t)len * PAIRS)[q] = ck_make(rk[j] & CK_ID, 0u);
-      ++len;
-    }
+  sort_ranked(rk, wc);
+  cache_update_lane(a.ckey, PAIRS, q, rk, c, wc, len, up, errf);
 }
 
 // ---- consume, wave path (16 < c <= 64): all lanes on pair q; len/up wave-uniform ----
 __device__ inline void consume_wave(const CgArgs& a, uint32_t q, uint32_t c, uint32_t& len, uint32_t& up,
                                     uint32_t* scr, uint32_t& errf) {
-  const size_t PAIRS = a.PAIRS;
   const uint32_t l = lane_id();
-  uint32_t key = l < c ? (a.inb + (size_t)l * PAIRS)[q] : 0xFFFFFFFFu;
-#pragma unroll
-  for (uint32_t k = 2; k <= 64; k <<= 1)  // bitonic sort across the wave, ascending by lane
-#pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      const uint32_t other = (uint32_t)__shfl_xor((int)key, (int)j);
-      const bool asc = (l & k) == 0;
-      const bool lower = (l & j) == 0;
-      key = (lower == asc) ? min(key, other) : max(key, other);
-    }
-  const uint32_t src = key & CK_ID;
-  const uint32_t L0 = len;
-  for (uint32_t i = l; i < L0; i += 64) scr[i] = (a.ckey + (size_t)i * PAIRS)[q];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  int found = -1;
-  if (l < c)
-    for (uint32_t i = 0; i < L0; ++i)
-      if (ck_id(scr[i]) == src) found = (int)i;
-  const bool isnew = l < c && found < 0;
-  const uint64_t nb = __ballot(isnew);
-  const uint32_t n0 = (uint32_t)(nb & 1u), n1 = (uint32_t)((nb >> 1) & 1u);
-  up = up < 255 ? up + 1 : 255;
-  if (l < 2) {
-    if (found >= 0) {
-      (a.ckey + (size_t)found * PAIRS)[q] = ck_bump(scr[found]);
-    } else {
-      const uint32_t pos = L0 + (l == 1 ? n0 : 0u);
-      if (pos < CACHE_CAP) (a.ckey + (size_t)pos * PAIRS)[q] = ck_make(src, 1u);
-      else errf |= ERR_CACHE;
-    }
-  }
-  const uint32_t L1 = min(L0 + n0 + n1, CACHE_CAP);
-  const uint64_t rest = nb & ~3ull;
-  if (l >= 2 && isnew) {
-    const uint32_t pos = L1 + (uint32_t)__popcll(rest & ((1ull << l) - 1));
-    if (pos < CACHE_LIMIT) (a.ckey + (size_t)pos * PAIRS)[q] = ck_make(src, 0u);
-  }
-  const uint32_t nrest = (uint32_t)__popcll(rest);
-  len = L1 + (L1 < CACHE_LIMIT ? min(nrest, CACHE_LIMIT - L1) : 0u);
+  const uint32_t key = wave_sort(l < c ? (a.inb + (size_t)l * a.PAIRS)[q] : 0xFFFFFFFFu);
+  cache_update_wave(a.ckey, a.PAIRS, q, key, c, len, up, scr, errf);
 }
 
 // ---- consume, any in-degree (c > 64): lane 0, records selected in order ----
 __device__ inline void consume_serial(const CgArgs& a, uint32_t q, uint32_t c, uint32_t& len, uint32_t& up,
                                       uint32_t& errf) {
   const size_t PAIRS = a.PAIRS;
-  uint32_t ln = len, u = up;
-  if (lane_id() == 0) {
-    uint32_t prev = 0;
-    u = u < 255 ? u + 1 : 255;
-    for (uint32_t k = 0; k < c; ++k) {
-      uint32_t best = 0xFFFFFFFFu;
-      for (uint32_t j = 0; j < c; ++j) {
-        const uint32_t r = a.inb[(size_t)j * PAIRS + q];
-        if ((k == 0 || r > prev) && r < best) best = r;
-      }
-      prev = best;
-      const uint32_t src = best & CK_ID;
-      int found = -1;
-      for (uint32_t i = 0; i < ln; ++i)
-        if (ck_id(a.ckey[(size_t)i * PAIRS + q]) == src) { found = (int)i; break; }
-      if (k < 2) {
-        if (found >= 0) {
-          uint32_t* sp = a.ckey + (size_t)found * PAIRS + q;
-          *sp = ck_bump(*sp);
-        } else if (ln < CACHE_CAP) {
-          a.ckey[(size_t)ln * PAIRS + q] = ck_make(src, 1u);
-          ++ln;
-        } else {
-          errf |= ERR_CACHE;
-        }
-      } else if (found < 0 && ln < CACHE_LIMIT) {
-        a.ckey[(size_t)ln * PAIRS + q] = ck_make(src, 0u);
-        ++ln;
-      }
+  cache_update_serial(a.ckey, PAIRS, q, c, len, up, errf, [&](uint32_t k, uint32_t prev) {
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t j = 0; j < c; ++j) {
+      const uint32_t r = a.inb[(size_t)j * PAIRS + q];
+      if ((k == 0 || r > prev) && r < best) best = r;
     }
-  }
-  len = (uint32_t)__shfl((int)ln, 0);
-  up = (uint32_t)__shfl((int)u, 0);
+    return best;
+  });
 }
 
 // After a pair's consume: record its in-degree, queue a due prune, else clear the
@@ -441,7 +328,7 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
 }  // namespace
 
 // consume_messages + send_prunes + prune_connections of every slot (gs_round's step path).
-hipError_t launch_consume_prune_g(Engine& e, bool record) {
+hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume) {
   CgArgs a;
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
   a.min_ingress = e.min_ingress; a.thr = e.thr; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake;
@@ -457,7 +344,7 @@ hipError_t launch_consume_prune_g(Engine& e, bool record) {
   a.wave_c = narrow ? 8u : 64u;
   // (slot_prunes was zeroed by launch_consume_prune)
   const uint32_t grid = (uint32_t)std::min<size_t>((e.PAIRS + CG_THREADS - 1) / CG_THREADS, 8192);
-  hipLaunchKernelGGL(k_cg_consume, dim3(grid), dim3(CG_THREADS), 0, e.st, a);
+  if (consume) hipLaunchKernelGGL(k_cg_consume, dim3(grid), dim3(CG_THREADS), 0, e.st, a);
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_cg_prune<A>, dim3(grid), dim3(CG_THREADS), 0, e.st, a));
   return hipGetLastError();
 }

@@ -271,6 +271,7 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   if (mode == GS_BFS_MULTI) {
     const MvGeom& g = e->mv;
     if (const char* dg = std::getenv("GS_MV_DIAG"); dg && dg[0] == '1') e->mv_diag = true;
+    if (const char* fu = std::getenv("GS_MV_FUSED"); fu && fu[0] == '0') e->mv_fused = false;
     e->ORW = ((e->ASZP + 1 + e->ASZP / 4) + 3) & ~3u;  // row, meta, the peers' failure classes
     ALLOC(e->own, N * e->ORW, 0);
     ALLOC(e->mv_vis, N, 0);
@@ -510,10 +511,11 @@ static int flush_rot_clear(Engine* e) {
 }
 
 static int do_bfs(Engine* e, bool record) {
-  hipEvent_t t0;
-  e->tbegin("bfs", &t0);
+  hipEvent_t t0 = nullptr;
+  const bool self_timed = e->bfs_mode == GS_BFS_MULTI;  // times its levels and its gather itself
+  if (!self_timed) e->tbegin("bfs", &t0);
   hipError_t r = launch_bfs(*e, record);
-  e->tend("bfs", t0);
+  if (!self_timed) e->tend("bfs", t0);
   e->inb_valid = true;
   if (r == hipErrorNotSupported) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
   HIPC(r);
@@ -602,8 +604,21 @@ int gs_round(gs_engine* eh, uint32_t round, int record) {
     return GS_OK;
   }
   if (int s = flush_rot_clear(e)) return s;
-  if (int s = do_bfs(e, rec)) return s;
-  if (int s = do_cp(e, true, true, true, rec)) return s;
+  if (e->bfs_mode == GS_BFS_MULTI && e->mv_fused) {  // gather fused with consume: the inbound rows stay on-chip
+    hipError_t r = launch_bfs_multi(*e, rec, true);
+    e->inb_valid = false;
+    if (r == hipErrorNotSupported) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
+    HIPC(r);
+    hipEvent_t t0;
+    e->tbegin("consume", &t0);
+    r = hipMemsetAsync(e->slot_prunes, 0, e->S * 4, e->st);
+    if (r == hipSuccess) r = launch_consume_prune_g(*e, rec, false);
+    e->tend("consume", t0);
+    HIPC(r);
+  } else {
+    if (int s = do_bfs(e, rec)) return s;
+    if (int s = do_cp(e, true, true, true, rec)) return s;
+  }
   if (int s = gs_chance_to_rotate(eh, round)) return s;
   if (rec) return do_stats(e, e->bfs_mode == GS_BFS_WORKGROUP ? 2 : e->bfs_mode == GS_BFS_MULTI ? 4 : 1);
   return GS_OK;
@@ -627,8 +642,8 @@ int gs_read_inbound(gs_engine* eh, uint32_t slot, uint32_t* off, uint32_t* src, 
   SLOT_CHECK(slot);
   if (int s = check_err(e)) return s;
   if (!e->inb_valid)
-    return fail(GS_ESTATE, "inbound records are kept on-chip by the one-kernel gs_round; "
-                           "call gs_run_gossip to materialize them");
+    return fail(GS_ESTATE, "inbound records are kept on-chip by gs_round (the one-kernel round, or the "
+                           "multi-source BFS's fused gather + consume); call gs_run_gossip to materialize them");
   const size_t N = e->N, base = (size_t)slot * N;
   std::vector<uint32_t> cnt(N), recs(N * e->capin);
   HIPC(hipMemcpyAsync(cnt.data(), e->cnt + base, N * 4, hipMemcpyDeviceToHost, e->st));
@@ -950,8 +965,8 @@ int gs_read_mst(gs_engine* eh, uint32_t slot, uint32_t* parent) {
   SLOT_CHECK(slot);
   if (!parent) return fail(GS_EINVAL, "null argument");
   if (!e->inb_valid)
-    return fail(GS_ESTATE, "inbound records are kept on-chip by the one-kernel gs_round; "
-                           "call gs_run_gossip to materialize them");
+    return fail(GS_ESTATE, "inbound records are kept on-chip by gs_round (the one-kernel round, or the "
+                           "multi-source BFS's fused gather + consume); call gs_run_gossip to materialize them");
   if (e->N > (1u << 18)) return fail(GS_ERANGE, "gs_read_mst is a debug readback for n <= 262,144");
   const uint32_t N = e->N, org = e->slots[slot].origin;
   std::vector<uint8_t> hops(N);

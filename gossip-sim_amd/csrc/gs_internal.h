@@ -32,7 +32,7 @@ struct BinGeom {
 // records u64 = src | node-in-bin << UB | slot mask << (UB + BS), slot groups of <= GW.
 constexpr uint32_t GT_WORDS = 96;  // per-group table words
 struct MvGeom {
-  uint32_t UB = 0, BSC = 0, BSF = 0, nbc = 0, nbf = 0, GW = 0, TW = 0, gcap = 0;
+  uint32_t UB = 0, BSC = 0, BSF = 0, nbc = 0, nbf = 0, GW = 0, TW = 0, gcap = 0, gcap_c = 0;
   size_t q_cap = 0, area_cap = 0, rows_cap = 0, pcap = 0;
 };
 struct MvGroup { uint32_t s0, sg, seed0, nseed; };
@@ -123,6 +123,7 @@ struct Engine {
   hipEvent_t mv_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool mv_attr_set = false;
   bool mv_diag = false;  // GS_MV_DIAG=1
+  bool mv_fused = true;  // gs_round: fused gather + consume (GS_MV_FUSED=0: gather, then k_cg_consume)
   std::vector<uint32_t> h_nfail_any;  // host copy: slot has failed nodes
   // rotation
   uint32_t* rot_list = nullptr;
@@ -197,12 +198,14 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
 bool mv_supported(const MvGeom& g, uint32_t ASZP);
 void mv_build_groups(Engine& e, const std::vector<uint32_t>& origins, const std::vector<uint8_t>& obkt,
                      const std::vector<uint8_t>& bucket, std::vector<uint32_t>& gtab, std::vector<uint2>& seeds);
-hipError_t launch_bfs_multi(Engine& e, bool record);
+// consume: gs_round's fused gather + consume (k_mv_consume) instead of the materializing
+// gather; then only k_cg_prune remains (launch_consume_prune_g(e, record, false)).
+hipError_t launch_bfs_multi(Engine& e, bool record, bool consume = false);
 hipError_t mv_update_failures(Engine& e, const std::vector<uint32_t>& nf);
 // own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
-hipError_t launch_consume_prune_g(Engine& e, bool record);
+hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume = true);
 // node-range partition (gs_partition.hip)
 size_t part_stats_words(const Engine& e);
 hipError_t launch_part_begin(Engine& e);

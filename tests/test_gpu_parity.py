@@ -610,6 +610,8 @@ def test_c4_sweep_slots_1m():
                 np.testing.assert_array_equal(x, y)
             for x, y in zip(aa, b.accumulators(k)):
                 np.testing.assert_array_equal(x, y)
+    for e in engs:  # gs_round keeps the multi BFS's inbound rows on-chip: materialize the next BFS
+        e.run_gossip()
     for k in (0, 12):
         ia = a.inbound(k, cap=32 * n)
         for b in engs[1:]:
@@ -648,9 +650,13 @@ def test_c3_widest_rows_100k():
         np.testing.assert_array_equal(sa, b.summaries())
     for k in range(2):
         ha = _invariants(a, k, n, sa[-1, k])
-        ia = a.inbound(k, cap=32 * n)
         for b in engs[1:]:
             np.testing.assert_array_equal(ha, b.hops(k))
+    for e in engs:  # gs_round keeps the multi BFS's inbound rows on-chip: materialize the next BFS
+        e.run_gossip()
+    for k in range(2):
+        ia = a.inbound(k, cap=32 * n)
+        for b in engs[1:]:
             for x, y in zip(ia, b.inbound(k, cap=32 * n)):
                 np.testing.assert_array_equal(x, y)
 
