@@ -74,16 +74,12 @@ EXPORTS = {
     "gs_last_error": (C.c_char_p, []),
     "gs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "gs_read_mst": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
-    "gs_part_attach": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
-    "gs_part_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t),
-                                C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
-    "gs_part_begin": (C.c_int, [C.c_void_p]),
-    "gs_part_level": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
-    "gs_part_frontier_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
-    "gs_part_frontier_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
-    "gs_part_consume": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
-    "gs_part_delta_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
-    "gs_part_delta_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "gs_create_part": (C.c_int, [C.POINTER(Params), C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                 C.POINTER(C.c_void_p)]),
+    "gs_part_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "gs_part_round": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.POINTER(C.c_uint32)]),
+    "gs_part_prunes_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "gs_part_prunes_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),
     "gs_part_stats_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_part_stats_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_create": (C.c_int, [C.POINTER(Params), C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p)]),
@@ -120,6 +116,7 @@ EXPORTS = {
     "gs_kernel_time": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "gs_kernel_time_reset": (C.c_int, [C.c_void_p]),
     "gs_engine_round_kind": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "gs_engine_memory": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "gs_engine_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_uint64)]),
     "gs_hops_stat_new": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p]),
@@ -188,7 +185,7 @@ class Engine:
 
     def __init__(self, stakes, n_slots, *, fanout=6, active_set_size=12, rotation_probability=0.013333, seed=0,
                  device=0, bfs_mode=GS_BFS_AUTO, inbound_capacity=0, profile=False, split_round=False,
-                 narrow_wave_path=False, binned_all_levels=False, wide_records=False):
+                 narrow_wave_path=False, binned_all_levels=False, wide_records=False, part=None):
         L = lib()
         self.stakes = np.ascontiguousarray(stakes, dtype=np.uint64)
         self.n = len(self.stakes)
@@ -200,7 +197,10 @@ class Engine:
                    (GS_FLAG_BINNED_ALL_LEVELS if binned_all_levels else 0) |
                    (GS_FLAG_WIDE_RECORDS if wide_records else 0))
         h = C.c_void_p()
-        _check(L.gs_create(C.byref(p), _ptr(self.stakes), self.n, n_slots, C.byref(h)))
+        if part is None:
+            _check(L.gs_create(C.byref(p), _ptr(self.stakes), self.n, n_slots, C.byref(h)))
+        else:  # (rank, nranks): one rank of a node-range partition (gossip_sim_amd.partition)
+            _check(L.gs_create_part(C.byref(p), _ptr(self.stakes), self.n, n_slots, part[0], part[1], C.byref(h)))
         self.h = h
 
     def close(self):
@@ -216,8 +216,10 @@ class Engine:
         _check(lib().gs_engine_info(self.h, C.byref(n), C.byref(s), C.byref(m), C.byref(b)))
         f = C.c_uint32()
         _check(lib().gs_engine_round_kind(self.h, C.byref(f)))
+        pb, ob = C.c_uint64(), C.c_uint64()
+        _check(lib().gs_engine_memory(self.h, C.byref(pb), C.byref(ob)))
         return {"n_nodes": n.value, "n_slots": s.value, "bfs_mode": m.value, "device_bytes": b.value,
-                "fused_round": bool(f.value)}
+                "pair_bytes": pb.value, "other_bytes": ob.value, "fused_round": bool(f.value)}
 
     def set_slots(self, origins, min_ingress=2, thresholds=0.15):
         S = self.n_slots

@@ -64,7 +64,7 @@ struct MvArgs {
   uint8_t* hops;
   uint32_t* cnt;
   uint32_t* inb;
-  uint8_t* egress;        // node-major [N][SP]
+  uint8_t* egress;        // node-major [NP][SP] (nodes [vlo, vhi))
   uint32_t* err;
   uint32_t* vis;          // [N] slot masks reached
   uint32_t* lvl;          // [256] frontier entries per level
@@ -72,15 +72,19 @@ struct MvArgs {
   uint32_t* T;            // [rows_cap][TW] rows of the current level
   unsigned long long* area;  // records of the current level
   uint32_t* ctr;          // [0] records used in area (this level)
-  unsigned long long* pool;  // [nbf][pcap] records of the round, per fine bin, level runs
-  uint32_t* pused;        // [nbf] records in each fine bin's pool region
-  uint2* Lt;              // [256][nbf] (pool start, count) of fine bin f at level d
+  unsigned long long* pool;  // [fno][pcap] records of the round, per (kept) fine bin, level runs
+  uint32_t* pused;        // [fno] records in each fine bin's pool region
+  uint2* Lt;              // [256][fno] (pool start, count) of fine bin flo + i at level d
   uint32_t* cmeta;        // fused consume (gs_round): the received caches, as in gs_consume_g.hip
   uint32_t* ckey;
   uint8_t* prune_round;
   uint32_t* ingress_acc;
   uint32_t N, SP, ASZ, fanout, capin, s0, Sg, UB, BSC, BSF, nbc, nbf, TW, ORW, any_fail, gcap, gcap_c;
   uint32_t lane_c, wave_c, record;
+  // nodes with per-pair state [vlo, vhi) (= fine bins [flo, flo + fno)); pair = slot * NP + node - vlo.
+  // A node-range partition rank runs the whole BFS but keeps the records, counts and
+  // egress of its own nodes only.
+  uint32_t vlo, vhi, flo, fno, NP;
   size_t PAIRS, area_cap, rows_cap, q_cap, pcap;
 };
 
@@ -169,7 +173,8 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const uint32_
   const uint32_t org0 = sorg[0];
   uint32_t tk0 = 0, msh = 0;
   bool have0 = false;
-  uint8_t* eg = a.egress + (size_t)u * a.SP + a.s0;
+  const bool own_u = u - a.vlo < a.vhi - a.vlo;  // egress is kept for owned nodes
+  uint8_t* eg = a.egress + (size_t)(u - a.vlo) * a.SP + a.s0;
 #pragma unroll
   for (uint32_t q = 0; q < MV_SG4; ++q) {
     if (q >= nq) break;
@@ -202,7 +207,8 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const uint32_
       }
       egw |= (uint32_t)__popc(tk) << (8 * t);
     }
-    if (mq4 == 0xFu) {
+    if (!own_u) {
+    } else if (mq4 == 0xFu) {
       *reinterpret_cast<uint32_t*>(eg + 4 * q) = egw;  // SP and s0 are multiples of 4
     } else {
 #pragma unroll
@@ -222,7 +228,8 @@ __global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, const
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t sorg[32], sfk[32], sbase;
   const uint32_t qn = a.lvl[d];
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.hlvl[d] = qn;  // the host's termination poll
+  if (blockIdx.x == 0 && threadIdx.x == 0)  // the host's termination poll (host-mapped)
+    __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint32_t G = (qn + MV_XT - 1) / MV_XT;
   if (blockIdx.x >= G) return;  // idle workgroups leave before any setup
   if (G > a.rows_cap) {
@@ -366,7 +373,7 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint2*
       uint32_t vl = (uint32_t)(rec >> UB) & BPm;
       if (live && GS_OOB(vl, nv, a.err, "multi record node")) vl = 0;
       if (live) atomicOr(&visL[vl], (uint32_t)(rec >> (UB + BSC)));
-      const uint32_t fb = live ? vl >> a.BSF : 0xFFFFu;
+      const uint32_t fb = live && f0 + (vl >> a.BSF) - a.flo < a.fno ? vl >> a.BSF : 0xFFFFu;  // kept bins only
       uint32_t pos = 0;
       for (uint32_t k = 0; k < NF; ++k) {  // one LDS atomic per wave and fine bin
         const uint64_t m = __ballot(fb == k);
@@ -377,20 +384,22 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint2*
         base = (uint32_t)__shfl((int)base, (int)leader);
         if (fb == k) pos = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
       }
-      if (live) {
-        const size_t pp = (size_t)a.pused[f0 + fb] + pos;
-        if (pp < a.pcap) a.pool[(size_t)(f0 + fb) * a.pcap + pp] = rec;
+      if (fb != 0xFFFFu) {
+        const uint32_t fl = f0 + fb - a.flo;
+        const size_t pp = (size_t)a.pused[fl] + pos;
+        if (pp < a.pcap) a.pool[(size_t)fl * a.pcap + pp] = rec;
       }
     }
     __syncthreads();
   }
   __syncthreads();
-  if (tid < NF) {  // the level's run of each fine bin, for the gather
-    const uint32_t used = a.pused[f0 + tid], n = fcur[tid];
+  if (tid < NF && f0 + tid - a.flo < a.fno) {  // the level's run of each kept fine bin, for the gather
+    const uint32_t fl = f0 + tid - a.flo;
+    const uint32_t used = a.pused[fl], n = fcur[tid];
     const bool over = (size_t)used + n > a.pcap;
     if (over) atomicOr(a.err, ERR_MV_CAP);
-    a.Lt[(size_t)d * a.nbf + f0 + tid] = make_uint2(used, over ? 0u : n);
-    a.pused[f0 + tid] = over ? used : used + n;
+    a.Lt[(size_t)d * a.fno + fl] = make_uint2(used, over ? 0u : n);
+    a.pused[fl] = over ? used : used + n;
   }
   if (!loaded) return;  // no records: no first arrivals in this bin
   // first arrivals (hop d + 1) become next-level entries, in node order
@@ -444,7 +453,7 @@ __device__ inline T mv_ld(T* p) {  // device-scope load: lines updated by atomic
 template <int ASZP>
 __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2* __restrict__ q0,
                                                     uint2* __restrict__ q1, uint32_t* __restrict__ hstate) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t snap[];  // [nbf] pool fill at level start
+  extern __shared__ __attribute__((aligned(16))) uint32_t snap[];  // [fno] pool fill at level start
   __shared__ uint32_t sorg[32], sfk[32], gt[GT_WORDS], cnt_s;
   const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BPm = (1u << BSC) - 1;
   if (tid < a.Sg) {
@@ -456,10 +465,10 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2
   while (qn > 0 && qn <= MV_SMALL && d < 254) {
     uint2* qcur = (d & 1) ? q1 : q0;
     uint2* qnxt = (d & 1) ? q0 : q1;
-    for (uint32_t f = tid; f < a.nbf; f += MV_ST) snap[f] = mv_ld(&a.pused[f]);
+    for (uint32_t f = tid; f < a.fno; f += MV_ST) snap[f] = mv_ld(&a.pused[f]);
     if (tid == 0) {
       cnt_s = 0;
-      a.hlvl[d] = qn;
+      __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
     for (uint32_t i0 = 0; i0 < qn; i0 += MV_ST) {
@@ -468,18 +477,29 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
       if (i < qn) mv_expand_entry<ASZP>(a, qcur[i], sorg, sfk, row, acc, u);
+      // every atomic of the entry is issued before any result is used (one wait, not
+      // one round trip per pushed-to peer)
+      uint32_t old[ASZP], pp[ASZP];
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) old[s] = acc[s] ? atomicOr(&a.vis[row[s]], acc[s]) : 0xFFFFFFFFu;
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        const uint32_t f = (row[s] >> a.BSF) - a.flo;
+        pp[s] = acc[s] && f < a.fno ? atomicAdd(&a.pused[f], 1u) : 0xFFFFFFFFu;  // kept bins only
+      }
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) {
         if (!acc[s]) continue;
         const uint32_t w = row[s];
-        const uint32_t nw = acc[s] & ~atomicOr(&a.vis[w], acc[s]);
-        const uint32_t f = w >> a.BSF;
-        const uint32_t p = atomicAdd(&a.pused[f], 1u);
-        if (p < a.pcap)
-          a.pool[(size_t)f * a.pcap + p] = (unsigned long long)u | ((unsigned long long)(w & BPm) << UB) |
-                                           ((unsigned long long)acc[s] << (UB + BSC));
-        else
-          atomicOr(a.err, ERR_MV_CAP);
+        const uint32_t nw = acc[s] & ~old[s];
+        if (pp[s] != 0xFFFFFFFFu) {
+          const uint32_t f = (w >> a.BSF) - a.flo;
+          if (pp[s] < a.pcap)
+            a.pool[(size_t)f * a.pcap + pp[s]] = (unsigned long long)u | ((unsigned long long)(w & BPm) << UB) |
+                                                 ((unsigned long long)acc[s] << (UB + BSC));
+          else
+            atomicOr(a.err, ERR_MV_CAP);
+        }
         if (nw) {  // this thread's first arrivals at w (another thread may add more bits to w)
           const uint32_t bw = a.bucket[w];
           const uint32_t n = mv_parts(gt, w, nw, bw, nullptr, 0);
@@ -490,16 +510,16 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2
       }
     }
     __syncthreads();
-    for (uint32_t f = tid; f < a.nbf; f += MV_ST)  // the level's pool run of every fine bin
-      a.Lt[(size_t)d * a.nbf + f] = make_uint2(snap[f], mv_ld(&a.pused[f]) - snap[f]);
+    for (uint32_t f = tid; f < a.fno; f += MV_ST)  // the level's pool run of every kept fine bin
+      a.Lt[(size_t)d * a.fno + f] = make_uint2(snap[f], mv_ld(&a.pused[f]) - snap[f]);
     qn = min(cnt_s, (uint32_t)a.q_cap);
     ++d;
     if (tid == 0) a.lvl[d] = qn;
     __syncthreads();
   }
   if (tid == 0) {
-    hstate[0] = d;
-    hstate[1] = qn;
+    __hip_atomic_store(&hstate[1], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hstate[0], d, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // the host polls this word
   }
 }
 
@@ -519,7 +539,7 @@ struct MvCsr {
   uint32_t *rs, *rp, *cn, *cur, *ctl, *sorg, *keys, *msk;
 };
 
-// After the last level, per fine bin f: the bin's records of every level (its pool runs,
+// After the last level, per kept fine bin f (local index; node base v0): the bin's records of every level (its pool runs,
 // in level order) as an LDS CSR by destination. Nodes whose records exceed gcap are
 // taken in consecutive ranges; body(lo, hi, base) runs on each range (all threads; no
 // barrier inside body is needed, one follows it).
@@ -529,7 +549,7 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, ui
   const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BSF = a.BSF, BP = 1u << BSF, BPm = BP - 1;
   const uint32_t um = (1u << UB) - 1;
   uint32_t *rs = L.rs, *rp = L.rp, *cn = L.cn, *cur = L.cur, *ctl = L.ctl, *keys = L.keys, *msk = L.msk;
-  const unsigned long long* pool = a.pool + (size_t)f * a.pcap;
+  const unsigned long long* pool = a.pool + (size_t)f * a.pcap;  // (f: local kept-bin index)
   for (uint32_t i = tid; i <= BP; i += MV_GT) cn[i] = 0;
   if (tid < a.Sg) L.sorg[tid] = a.origin[a.s0 + tid];
   {  // the run table: thread d reads level d's (start, count); exclusive prefix of the counts
@@ -537,7 +557,7 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, ui
     if (tid < 256) {
       rs[tid] = 0;
       if (tid < nlev && a.lvl[tid]) {  // an empty level wrote no run
-        const uint2 R = a.Lt[(size_t)tid * a.nbf + f];
+        const uint2 R = a.Lt[(size_t)tid * a.fno + f];
         rs[tid] = R.x;
         n = R.y;
       }
@@ -641,33 +661,101 @@ __device__ inline MvCsr mv_csr_lds(unsigned char* smem, uint32_t BP, uint32_t gc
   return L;
 }
 
+// Slot j's records of one node (list r0 .. r1 of the bin's CSR): the count c and the
+// first 16 matches in list order in rk[0 .. min(c, 16)) (~0 beyond). A list of <= 64
+// records is filtered to a bitmap (one LDS load and two ALU ops per record), then the
+// matches are extracted in lockstep over the wave (t = 0, 1, ...: no per-lane register
+// index); a longer list collects its matches record by record. All lanes of the wave
+// must be active (the extraction bound is a wave maximum).
+__device__ inline void mv_pair_records(const MvCsr& L, uint32_t r0, uint32_t r1, uint32_t j, uint32_t (&rk)[16],
+                                       uint32_t& c) {
+#pragma unroll
+  for (int t = 0; t < 16; ++t) rk[t] = 0xFFFFFFFFu;
+  const uint32_t Ln = r1 - r0;
+  uint32_t blo = 0, bhi = 0;
+  c = 0;
+  if (Ln <= 64) {
+    const uint32_t l1 = min(Ln, 32u);
+    for (uint32_t k = 0; k < l1; ++k) blo |= ((L.msk[r0 + k] >> j) & 1u) << k;
+    for (uint32_t k = 32; k < Ln; ++k) bhi |= ((L.msk[r0 + k] >> j) & 1u) << (k - 32);
+    c = (uint32_t)(__popc(blo) + __popc(bhi));
+  } else {
+    for (uint32_t r = r0; r < r1; ++r) {
+      if (!((L.msk[r] >> j) & 1u)) continue;
+      const uint32_t key = L.keys[r];
+#pragma unroll
+      for (int t = 0; t < 16; ++t) rk[t] = c == (uint32_t)t ? key : rk[t];
+      ++c;
+    }
+  }
+  const uint32_t wx = active_max<5>(min(c, 16u));
+#pragma unroll
+  for (uint32_t t = 0; t < 16; ++t) {
+    if (t >= wx) break;
+    if (blo | bhi) {
+      const uint32_t pos = blo ? (uint32_t)__builtin_ctz(blo) : 32u + (uint32_t)__builtin_ctz(bhi);
+      if (blo) blo &= blo - 1; else bhi &= bhi - 1;
+      rk[t] = L.keys[r0 + pos];
+    }
+  }
+}
+
+// The smallest hop among slot j's records of the node (rk holds them all when c <= 16).
+__device__ inline uint32_t mv_pair_hop(const MvCsr& L, uint32_t r0, uint32_t r1, uint32_t j, const uint32_t (&rk)[16],
+                                       uint32_t c) {
+  uint32_t mh = 0xFFu;
+  if (c <= 16) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) mh = min(mh, rk[t] >> 24);
+  } else {
+    for (uint32_t r = r0; r < r1; ++r)
+      if ((L.msk[r] >> j) & 1u) mh = min(mh, L.keys[r] >> 24);
+  }
+  return mh;
+}
+
 // Per (slot, node) of the fine bin: in-degree, the inbound rows and the hop, coalesced
 // over nodes (the step API's gs_run_gossip; gs_round fuses this with consume below).
+// Row t of every lane's pair is stored by one wave instruction (t = 0, 1, ...).
 __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t f = mv_xcd_bin(blockIdx.x, a.nbf);
-  if (f >= a.nbf) return;
-  const uint32_t tid = threadIdx.x, BP = 1u << a.BSF, Sg = a.Sg, v0 = f << a.BSF;
-  if (v0 >= a.N) return;
-  const uint32_t nv = min(BP, a.N - v0), gcap = a.gcap;
+  const uint32_t f = mv_xcd_bin(blockIdx.x, a.fno);  // local kept-bin index
+  if (f >= a.fno) return;
+  const uint32_t tid = threadIdx.x, BP = 1u << a.BSF, Sg = a.Sg, v0 = (a.flo + f) << a.BSF;
+  if (v0 >= a.vhi) return;
+  const uint32_t nv = min(BP, a.vhi - v0), gcap = a.gcap;
   const MvCsr L = mv_csr_lds(smem, BP, gcap);
   bool over = false;
   mv_bin_csr(a, f, nlev, nv, gcap, L, [&](uint32_t lo, uint32_t hi, uint32_t base) {
-    for (uint32_t i = lo + tid; i < hi; i += MV_GT) {
-      const uint32_t v = v0 + i, r0 = L.cn[i] - base, r1 = min(L.cn[i + 1] - base, gcap);
+    for (uint32_t i0 = lo; i0 < hi; i0 += MV_GT) {  // block-uniform trip count (whole waves below)
+      const uint32_t i = i0 + tid;
+      const bool in = i < hi;
+      const uint32_t v = v0 + i;
+      const uint32_t r0 = in ? L.cn[i] - base : 0u, r1 = in ? min(L.cn[i + 1] - base, gcap) : 0u;
       for (uint32_t j = 0; j < Sg; ++j) {
-        const size_t p = (size_t)(a.s0 + j) * a.N + v;
-        uint32_t cc = 0, mh = 0xFFu;
-        for (uint32_t r = r0; r < r1; ++r) {
-          if (!((L.msk[r] >> j) & 1u)) continue;
-          const uint32_t key = L.keys[r];
-          if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = key;
-          mh = min(mh, key >> 24);
-          ++cc;
+        const size_t p = (size_t)(a.s0 + j) * a.NP + (v - a.vlo);
+        uint32_t rk[16], cc;
+        mv_pair_records(L, r0, r1, j, rk, cc);
+        const uint32_t wc = min(active_max<7>(min(cc, 127u)), min(16u, a.capin));
+#pragma unroll
+        for (uint32_t t = 0; t < 16; ++t) {
+          if (t >= wc) break;
+          if (t < cc) a.inb[(size_t)t * a.PAIRS + p] = rk[t];
         }
-        over |= cc > a.capin;
-        a.cnt[p] = cc;
-        a.hops[p] = (uint8_t)(v == L.sorg[j] ? 0u : (cc ? mh : 0xFFu));
+        if (cc > 16) {  // (rare) rows 16 .. : the matches after the 16th, in list order
+          uint32_t k = 0;
+          for (uint32_t r = r0; r < r1; ++r) {
+            if (!((L.msk[r] >> j) & 1u)) continue;
+            if (k >= 16 && k < a.capin) a.inb[(size_t)k * a.PAIRS + p] = L.keys[r];
+            ++k;
+          }
+        }
+        const uint32_t mh = mv_pair_hop(L, r0, r1, j, rk, cc);
+        if (in) {
+          over |= cc > a.capin;
+          a.cnt[p] = cc;
+          a.hops[p] = (uint8_t)(v == L.sorg[j] ? 0u : (cc ? mh : 0xFFu));
+        }
       }
     }
   });
@@ -693,11 +781,11 @@ __device__ inline void mv_after_consume(const MvArgs& a, uint32_t q, uint32_t me
 // (records compacted by ballot, sorted across lanes), > wave_c by one lane.
 __global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void k_mv_consume(MvArgs a, uint32_t nlev) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t f = mv_xcd_bin(blockIdx.x, a.nbf);
-  if (f >= a.nbf) return;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, BP = 1u << a.BSF, Sg = a.Sg, v0 = f << a.BSF;
-  if (v0 >= a.N) return;
-  const uint32_t nv = min(BP, a.N - v0), gcap = a.gcap_c;
+  const uint32_t f = mv_xcd_bin(blockIdx.x, a.fno);  // local kept-bin index
+  if (f >= a.fno) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, BP = 1u << a.BSF, Sg = a.Sg, v0 = (a.flo + f) << a.BSF;
+  if (v0 >= a.vhi) return;
+  const uint32_t nv = min(BP, a.vhi - v0), gcap = a.gcap_c;
   uint32_t* wscr = reinterpret_cast<uint32_t*>(smem) + (tid >> 6) * MV_WSCR;  // [64] keys, [CACHE_CAP] cache
   const MvCsr L = mv_csr_lds(smem + MV_CSCR, BP, gcap);
   const size_t PAIRS = a.PAIRS;
@@ -709,50 +797,14 @@ __global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void
       const uint32_t v = v0 + i;
       const uint32_t r0 = in ? L.cn[i] - base : 0u, r1 = in ? min(L.cn[i + 1] - base, gcap) : 0u;
       for (uint32_t j = 0; j < Sg; ++j) {
-        const uint32_t q = (a.s0 + j) * a.N + v;
-        // the slot's records of the node: a list of <= 64 records is filtered to a bitmap
-        // (one bit per record), then its first 16 matches are extracted; a longer list
-        // collects them record by record
-        uint32_t rk[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) rk[t] = 0xFFFFFFFFu;
-        const uint32_t Ln = r1 - r0;
-        uint32_t c = 0, mh = 0xFFu, blo = 0, bhi = 0;
-        if (Ln <= 64) {
-          const uint32_t l1 = min(Ln, 32u);
-          for (uint32_t k = 0; k < l1; ++k) blo |= ((L.msk[r0 + k] >> j) & 1u) << k;
-          for (uint32_t k = 32; k < Ln; ++k) bhi |= ((L.msk[r0 + k] >> j) & 1u) << (k - 32);
-          c = (uint32_t)(__popc(blo) + __popc(bhi));
-        } else {
-          for (uint32_t r = r0; r < r1; ++r) {
-            if (!((L.msk[r] >> j) & 1u)) continue;
-            const uint32_t key = L.keys[r];
-#pragma unroll
-            for (int t = 0; t < 16; ++t) rk[t] = c == (uint32_t)t ? key : rk[t];
-            ++c;
-          }
-        }
-        const uint32_t wx = active_max<5>(min(c, 16u));
-#pragma unroll
-        for (uint32_t t = 0; t < 16; ++t) {
-          if (t >= wx) break;
-          if (blo | bhi) {
-            const uint32_t pos = blo ? (uint32_t)__builtin_ctz(blo) : 32u + (uint32_t)__builtin_ctz(bhi);
-            if (blo) blo &= blo - 1; else bhi &= bhi - 1;
-            rk[t] = L.keys[r0 + pos];
-          }
-          mh = min(mh, rk[t] >> 24);
-        }
-        if (c > 16) {  // (rare) the hop over every match
-          mh = 0xFFu;
-          for (uint32_t r = r0; r < r1; ++r)
-            if ((L.msk[r] >> j) & 1u) mh = min(mh, L.keys[r] >> 24);
-        }
-        uint32_t meta = 0;
+        const uint32_t q = (a.s0 + j) * a.NP + (v - a.vlo);
+        const uint32_t meta = in ? ntl(&a.cmeta[q]) : 0u;  // in flight during the filter
+        uint32_t rk[16], c;
+        mv_pair_records(L, r0, r1, j, rk, c);
+        const uint32_t mh = mv_pair_hop(L, r0, r1, j, rk, c);
         if (in) {
           a.cnt[q] = c;
           a.hops[q] = (uint8_t)(v == L.sorg[j] ? 0u : (c ? mh : 0xFFu));
-          meta = ntl(&a.cmeta[q]);
           if (c > a.capin) { over = 1; c = a.capin; }
         }
         uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
@@ -760,8 +812,10 @@ __global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void
         if (in && !heavy) {
           if (c) {
             const uint32_t wc = active_max<5>(c);
+            uint32_t kc0[8];
+            cache_prefetch(a.ckey, PAIRS, q, len, kc0);
             sort_ranked(rk, wc);
-            cache_update_lane(a.ckey, PAIRS, q, rk, c, wc, len, up, errf);
+            cache_update_lane(a.ckey, PAIRS, q, rk, c, wc, kc0, len, up, errf);
           }
           mv_after_consume(a, q, meta, c, len, up);
         }
@@ -840,6 +894,11 @@ __global__ void k_mv_fcls(const uint32_t* __restrict__ frank, const uint32_t* __
 }  // namespace
 
 // ------------------------------------------------------------------ host ----
+// Fine bins with per-pair state: all, or a partition rank's (its range starts on a bin).
+uint32_t mv_kept_bins(const Engine& e) {
+  return (e.NP + (1u << e.mv.BSF) - 1) >> e.mv.BSF;
+}
+
 static uint32_t ceil_log2(size_t x) {
   uint32_t l = 0;
   while (((size_t)1 << l) < x) ++l;
@@ -940,6 +999,8 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.pool = e.mv_pool; a.pused = e.mv_pused; a.Lt = e.mv_Lt;
   a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
+  a.vlo = e.vlo; a.vhi = e.vlo + e.NP; a.NP = e.NP;
+  a.flo = e.vlo >> e.mv.BSF; a.fno = mv_kept_bins(e);
   a.ORW = e.ORW;
   a.any_fail = 0;
   for (uint32_t j = 0; j < gr.sg; ++j) a.any_fail |= e.h_nfail_any[gr.s0 + j] ? 1u : 0u;
@@ -953,6 +1014,25 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.PAIRS = e.PAIRS; a.area_cap = e.mv.area_cap; a.rows_cap = e.mv.rows_cap; a.q_cap = e.mv.q_cap;
   a.pcap = e.mv.pcap;
   return a;
+}
+
+// Host-mapped words the level loop polls: PENDING until the kernel that writes them
+// runs. The spin checks the stream now and then, so a stream that finished (or failed)
+// without writing the word ends the wait instead of hanging it.
+constexpr uint32_t MV_PENDING = 0xFFFFFFFFu;
+static hipError_t mv_wait(volatile uint32_t* p, hipStream_t st, uint32_t& out) {
+  for (uint64_t it = 1;; ++it) {
+    const uint32_t x = *p;
+    if (x != MV_PENDING) { out = x; return hipSuccess; }
+    if ((it & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) {
+        out = *p;
+        return out != MV_PENDING ? hipSuccess : hipErrorUnknown;
+      }
+      if (q != hipErrorNotReady) return q;
+    }
+  }
 }
 
 hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
@@ -973,19 +1053,18 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       return r;
     GS_ASZP_DISPATCH(e.ASZP, {
       r = hipFuncSetAttribute((const void*)k_mv_small<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(e.mv.nbf * 4));
+                              (int)(mv_kept_bins(e) * 4));
     });
     if (r != hipSuccess) return r;
-    for (int i = 0; i < 4; ++i)
-      if ((r = hipEventCreateWithFlags(&e.mv_ev[i], hipEventDisableTiming)) != hipSuccess) return r;
     e.mv_attr_set = true;
   }
   const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8;
-  const uint32_t ggrid = ((e.mv.nbf + 7) / 8) * 8;
+  const uint32_t fno = mv_kept_bins(e);
+  const uint32_t ggrid = ((fno + 7) / 8) * 8;
   const uint32_t xgrid = 2048;
   volatile uint32_t* hl = e.mv_hlvl;  // host-mapped: expand(d) writes lvl[d]
   volatile uint32_t* hs = e.mv_hlvl + 256;  // host-mapped: the small-level kernel's (level, entries)
-  const size_t lds_s = (size_t)e.mv.nbf * 4;
+  const size_t lds_s = (size_t)fno * 4;
   for (uint32_t g = 0; g < (uint32_t)e.mv_groups.size(); ++g) {
     const MvGroup& gr = e.mv_groups[g];
     MvArgs a = mv_args(e, gr, g);
@@ -994,17 +1073,16 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     e.tbegin("bfs", &t0);
     if ((r = hipMemsetAsync(e.mv_vis, 0, (size_t)e.N * 4, e.st))) return r;
     if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st))) return r;
-    if ((r = hipMemsetAsync(e.mv_pused, 0, (size_t)e.mv.nbf * 4, e.st))) return r;
+    if ((r = hipMemsetAsync(e.mv_pused, 0, (size_t)fno * 4, e.st))) return r;
     hipLaunchKernelGGL(k_mv_seed, dim3((gr.nseed + 255) / 256), dim3(256), 0, e.st, a, e.mv_seed + gr.seed0, gr.nseed,
                        e.mv_q[0]);
     uint32_t nlev = 0, d = 0;
     for (;;) {
       // small levels in one workgroup, until the frontier is empty or large
+      hs[0] = MV_PENDING;
       GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, d,
                                                   e.mv_q[0], e.mv_q[1], e.mv_hstate_dev));
-      if ((r = hipEventRecord(e.mv_ev[0], e.st))) return r;
-      if ((r = hipEventSynchronize(e.mv_ev[0]))) return r;
-      d = hs[0];
+      if ((r = mv_wait(hs, e.st, d))) return r;
       if (hs[1] == 0) { nlev = d; break; }
       if (d >= 254) return hipErrorNotSupported;  // frontier still non-empty after 254 levels
       // large levels: expand + apply; the frontier size of level x is polled two levels late
@@ -1012,13 +1090,13 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       bool done = false;
       for (;; ++d) {
         if (d >= 254) return hipErrorNotSupported;
+        hl[d] = MV_PENDING;
         GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, d,
                                                     e.mv_q[d & 1]));
-        if ((r = hipEventRecord(e.mv_ev[d & 3], e.st))) return r;
         hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, d, e.mv_q[(d + 1) & 1]);
         if (d >= dl + 2) {
-          if ((r = hipEventSynchronize(e.mv_ev[(d - 2) & 3]))) return r;
-          const uint32_t x = hl[d - 2];
+          uint32_t x = 0;
+          if ((r = mv_wait(hl + (d - 2), e.st, x))) return r;
           if (x == 0) { nlev = d + 1; done = true; break; }
           if (x <= MV_SMALL) { ++d; break; }  // levels d - 1, d are enqueued; small levels from d + 1
         }
@@ -1031,7 +1109,7 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     else hipLaunchKernelGGL(k_mv_gather, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a, nlev);
     e.tend(consume ? "gather_consume" : "gather", t0);
     if (e.mv_diag) {  // GS_MV_DIAG=1: entries and records of the group's BFS (diagnostics)
-      std::vector<uint32_t> pu(e.mv.nbf);
+      std::vector<uint32_t> pu(fno);
       if ((r = hipMemcpyAsync(pu.data(), e.mv_pused, pu.size() * 4, hipMemcpyDeviceToHost, e.st))) return r;
       if ((r = hipStreamSynchronize(e.st))) return r;
       size_t ent = 0, rec = 0, mx = 0;

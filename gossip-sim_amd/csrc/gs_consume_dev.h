@@ -13,19 +13,27 @@ namespace gs {
 template <class T>
 __device__ inline T ntl(const T* p) { return __builtin_nontemporal_load(p); }
 
-// Register path: rk[0..c) sorted ascending, rk[c..16) = ~0 (1 <= c <= 16); wc = the
-// wave's largest c (selects the match width). Rank 0 and 1 are timely (score += 1,
-// inserted regardless of the 50-key cap); later ranks are inserted while len < 50.
-// Presence is kept as per-rank lane masks (bool: one compare per (key, rank), the OR
-// runs on the scalar unit), the cache rows are streamed 8 at a time.
+// The first 8 cache rows of the lane's pair (rows >= len are not loaded): issued before
+// the records are sorted, so the sort hides their latency.
+__device__ inline void cache_prefetch(const uint32_t* __restrict__ ckey, size_t PAIRS, size_t q, uint32_t len,
+                                      uint32_t (&kc)[8]) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) kc[t] = (uint32_t)t < len ? ntl(&(ckey + (size_t)t * PAIRS)[q]) : 0u;
+}
+
 template <int NC>
 __device__ inline void cache_match(uint32_t* __restrict__ ckey, size_t PAIRS, size_t q, const uint32_t (&rid)[16],
-                                   uint32_t len, uint32_t wl, bool (&pr)[16], int& idx0, int& idx1, uint32_t& w0,
-                                   uint32_t& w1) {
+                                   uint32_t len, uint32_t wl, const uint32_t (&kc0)[8], bool (&pr)[16], int& idx0,
+                                   int& idx1, uint32_t& w0, uint32_t& w1) {
   for (uint32_t i0 = 0; i0 < wl; i0 += 8) {
     uint32_t kc[8];
+    if (i0 == 0) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) kc[t] = i0 + t < len ? ntl(&(ckey + (size_t)(i0 + t) * PAIRS)[q]) : 0u;  // own rows only
+      for (int t = 0; t < 8; ++t) kc[t] = kc0[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) kc[t] = i0 + t < len ? ntl(&(ckey + (size_t)(i0 + t) * PAIRS)[q]) : 0u;
+    }
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
@@ -39,9 +47,14 @@ __device__ inline void cache_match(uint32_t* __restrict__ ckey, size_t PAIRS, si
   }
 }
 
+// Register path: rk[0..c) sorted ascending, rk[c..16) = ~0 (1 <= c <= 16); wc = the
+// wave's largest c (selects the match width); kc0 = cache_prefetch of the pair. Rank 0
+// and 1 are timely (score += 1, inserted regardless of the 50-key cap); later ranks are
+// inserted while len < 50. Presence is kept as per-rank lane masks (bool: one compare
+// per (key, rank), the OR runs on the scalar unit), the cache rows are streamed 8 at a time.
 __device__ inline void cache_update_lane(uint32_t* __restrict__ ckey, size_t PAIRS, size_t q,
-                                         const uint32_t (&rk)[16], uint32_t c, uint32_t wc, uint32_t& len,
-                                         uint32_t& up, uint32_t& errf) {
+                                         const uint32_t (&rk)[16], uint32_t c, uint32_t wc,
+                                         const uint32_t (&kc0)[8], uint32_t& len, uint32_t& up, uint32_t& errf) {
   uint32_t rid[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) rid[j] = (uint32_t)j < c ? rk[j] & CK_ID : 0xFFFFFFFEu;  // never a cache id
@@ -51,9 +64,9 @@ __device__ inline void cache_update_lane(uint32_t* __restrict__ ckey, size_t PAI
   uint32_t w0 = 0, w1 = 0;
   int idx0 = -1, idx1 = -1;
   const uint32_t wl = active_max<7>(len);
-  if (wc <= 4) cache_match<4>(ckey, PAIRS, q, rid, len, wl, pr, idx0, idx1, w0, w1);
-  else if (wc <= 8) cache_match<8>(ckey, PAIRS, q, rid, len, wl, pr, idx0, idx1, w0, w1);
-  else cache_match<16>(ckey, PAIRS, q, rid, len, wl, pr, idx0, idx1, w0, w1);
+  if (wc <= 4) cache_match<4>(ckey, PAIRS, q, rid, len, wl, kc0, pr, idx0, idx1, w0, w1);
+  else if (wc <= 8) cache_match<8>(ckey, PAIRS, q, rid, len, wl, kc0, pr, idx0, idx1, w0, w1);
+  else cache_match<16>(ckey, PAIRS, q, rid, len, wl, kc0, pr, idx0, idx1, w0, w1);
   up = up < 255 ? up + 1 : 255;  // rank 0 (received_cache.rs:84-86)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {

@@ -48,11 +48,12 @@ struct CgArgs {
   uint32_t* ckey;
   uint8_t* prune_round;
   uint32_t* slot_prunes;
-  uint32_t* mask;  // prune bits land here: the masks, or a node-range partition's delta
+  uint32_t* mask;  // prune bits land here
   uint32_t* ingress_acc;
   uint32_t* prune_acc;
   uint32_t* err;
   uint32_t N, S, ASZ, capin;
+  uint32_t NP, vlo;  // pair q = slot * NP + (node - vlo)
   size_t mso, msu;  // prune-mask strides of (slot, node)
   uint32_t lane_c, lane_l, wave_c;  // register-path bounds (16, 16) and wave-consume bound (64);
                                     // GS_FLAG_NARROW_WAVE_PATH: (4, 4, 8), so small tests reach every path
@@ -71,8 +72,10 @@ __device__ inline void consume_lane(const CgArgs& a, uint32_t q, uint32_t c, uin
   asm volatile("" ::: "memory");
 #pragma unroll
   for (int j = 0; j < 16; ++j) rk[j] = (uint32_t)j < c ? rk[j] : 0xFFFFFFFFu;
+  uint32_t kc0[8];
+  cache_prefetch(a.ckey, PAIRS, q, len, kc0);
   sort_ranked(rk, wc);
-  cache_update_lane(a.ckey, PAIRS, q, rk, c, wc, len, up, errf);
+  cache_update_lane(a.ckey, PAIRS, q, rk, c, wc, kc0, len, up, errf);
 }
 
 // ---- consume, wave path (16 < c <= 64): all lanes on pair q; len/up wave-uniform ----
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
     const uint32_t meta = q < P ? ntl(&a.cmeta[q]) : 0u;
     const bool due = q < P && ((meta >> 8) & 0xFF) >= MIN_NUM_UPSERTS;
     if (!__ballot(due)) continue;
-    const uint32_t o = q / a.N, v = q - o * a.N;
+    const uint32_t o = q / a.NP, v = a.vlo + (q - o * a.NP);
     const uint32_t len = meta & 0xFF;
     const bool heavy = due && len > a.lane_l;
     uint32_t npr = 0;
@@ -315,7 +318,7 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
       const int l = __ffsll((long long)hv) - 1;
       hv &= hv - 1;
       const uint32_t hq = (uint32_t)__shfl((int)q, l);
-      const uint32_t ho = hq / a.N, hvn = hq - ho * a.N;
+      const uint32_t ho = hq / a.NP, hvn = a.vlo + (hq - ho * a.NP);
       const uint32_t hlen = (uint32_t)__shfl((int)len, l);
       const uint32_t hn = prune_wave<ASZP>(a, hq, ho, hvn, hlen);
       if (lane_id() == 0) finish_prune(a, hq, hlen, hn);
@@ -333,11 +336,12 @@ hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume) {
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
   a.min_ingress = e.min_ingress; a.thr = e.thr; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake;
   a.cnt = e.cnt; a.inb = e.inb; a.cmeta = e.cmeta; a.ckey = e.ckey; a.prune_round = e.prune_round;
-  a.slot_prunes = e.slot_prunes; a.mask = e.part_on ? e.part_delta : e.mask; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc;
+  a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc;
+  a.NP = e.NP; a.vlo = e.vlo;
   a.err = e.err;
   a.N = e.N; a.S = e.S; a.ASZ = e.ASZ; a.capin = e.capin; a.PAIRS = e.PAIRS; a.record = record ? 1 : 0;
-  a.mso = e.part_on ? e.N : e.mso;  // a partition's delta is slot-major
-  a.msu = e.part_on ? 1 : e.msu;
+  a.mso = e.mso;
+  a.msu = e.msu;
   const bool narrow = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) != 0;
   a.lane_c = narrow ? 4u : 16u;
   a.lane_l = narrow ? 4u : LANE_L;

@@ -78,12 +78,11 @@ static void destroy_engine(Engine* e) {
   if (e->st) hipStreamSynchronize(e->st);
   for (void* p : e->allocs) hipFree(p);
   if (e->h_err) hipHostFree(e->h_err);
+  if (e->part_in) hipFree(e->part_in);
   if (e->mv_hlvl) hipHostFree(e->mv_hlvl);
   for (auto& kv : e->timers)
     for (auto& pr : kv.second.ev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (hipEvent_t x : e->ev_pool) hipEventDestroy(x);
-  for (hipEvent_t x : e->mv_ev)
-    if (x) hipEventDestroy(x);
   if (e->st) hipStreamDestroy(e->st);
   delete e;
 }
@@ -151,7 +150,9 @@ int gs_device_count(int* n) {
   return GS_OK;
 }
 
-int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t n_slots, gs_engine** out) {
+// K == 1: an engine over all nodes; K > 1: rank `rank` of a node-range partition.
+static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t n_slots, uint32_t rank,
+                         uint32_t K, gs_engine** out) {
   if (!prm || !stakes || !out) return fail(GS_EINVAL, "null argument");
   *out = nullptr;
   if (n < 2 || n > GS_MAX_NODES) return fail(GS_EINVAL, "n_nodes must be in [2, 2^24-1]");
@@ -173,6 +174,8 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   e->prm = *prm;
   e->N = n;
   e->S = n_slots;
+  e->NP = n;
+  e->vlo = 0;
   e->PAIRS = (size_t)n * n_slots;
   e->ASZ = prm->active_set_size;
   e->ASZP = (e->ASZ + 3) & ~3u;
@@ -193,6 +196,27 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   const bool bin_ok = pairs <= (1ull << 28) && bin_supported(e->bin, e->fcap);
   mv_geometry(n, n_slots, e->ASZ, e->ASZP, e->mv);
   const bool mv_ok = mv_supported(e->mv, e->ASZP);
+  if (K > 1) {  // a partition rank runs the multi-source BFS over its replicated tables
+    if (mode != GS_BFS_AUTO && mode != GS_BFS_MULTI) {
+      destroy_engine(e);
+      return fail(GS_EINVAL, "a node-range partition runs bfs_mode GS_BFS_MULTI (or AUTO)");
+    }
+    mode = GS_BFS_MULTI;
+    const uint32_t C = (((n + K - 1) / K) + 1023) & ~1023u;  // whole 1,024-node bins per rank
+    const uint32_t lo = (uint32_t)std::min<uint64_t>(n, (uint64_t)rank * C), hi = std::min(n, lo + C);
+    if (lo >= hi) {
+      destroy_engine(e);
+      return fail(GS_EINVAL, "node-range partition: rank owns no nodes (ranges are multiples of 1,024 ids)");
+    }
+    e->part_on = true;
+    e->part_K = K;
+    e->part_rank = rank;
+    e->part_lo = lo;
+    e->part_hi = hi;
+    e->NP = hi - lo;
+    e->vlo = lo;
+    e->PAIRS = (size_t)e->NP * n_slots;
+  }
   if (mode == GS_BFS_AUTO)
     mode = (n <= 8192 && n_slots >= 64) ? GS_BFS_WORKGROUP : (bin_ok ? GS_BFS_BINNED : GS_BFS_LEVEL);
   if (mode == GS_BFS_BINNED && !bin_ok) {
@@ -212,11 +236,12 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
     return fail(GS_EINVAL, "bfs_mode");
   }
   e->bfs_mode = mode;
+  e->inb_valid = mode != GS_BFS_MULTI;  // multi: no inbound rows until a step-wise BFS
   // one-kernel round (gs_round): per-slot state in LDS, at most 160 KiB per workgroup
   e->fused = mode == GS_BFS_WORKGROUP && !(prm->flags & GS_FLAG_SPLIT_ROUND) &&
              round_wg_lds_bytes(n, e->fcap, e->ASZP) <= 160 * 1024;
 
-  const size_t N = n, S = n_slots, PAIRS = e->PAIRS;
+  const size_t N = n, S = n_slots, PAIRS = e->PAIRS, NP = e->NP;
   e->SP = (uint32_t)((S + 3) & ~(size_t)3);
   if (mode == GS_BFS_MULTI) {  // node-major masks / egress: a node's slots share one line
     e->mso = 1; e->msu = e->SP; e->eso = 1; e->esu = e->SP; e->mask_words = N * e->SP;
@@ -241,18 +266,20 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   ALLOC(e->thr, S, 0);
   ALLOC(e->nfail, S, 0);
   ALLOC(e->slot_prunes, S, 0);
+  ALLOC(e->mask, e->mask_words, 0);
+  size_t b0 = e->dev_bytes;  // per-(slot, node) state from here (a partition rank: its own nodes)
   ALLOC(e->hops, PAIRS, 0xFF);
   ALLOC(e->cnt, PAIRS, 0);
-  ALLOC(e->mask, e->mask_words, 0);
-  ALLOC(e->inb, (size_t)e->capin * PAIRS, 0);
+  if (mode != GS_BFS_MULTI) ALLOC(e->inb, (size_t)e->capin * PAIRS, 0);  // multi: on first use (ensure_inb)
   ALLOC(e->cmeta, PAIRS, 0);
   ALLOC(e->ckey, (size_t)CACHE_CAP * PAIRS, 0);
-  ALLOC(e->egress, std::max(PAIRS, N * e->esu), 0);
+  ALLOC(e->egress, std::max(PAIRS, NP * e->esu), 0);
   ALLOC(e->prune_round, PAIRS, 0);
   ALLOC(e->egress_acc, PAIRS, 0);
   ALLOC(e->ingress_acc, PAIRS, 0);
   ALLOC(e->prune_acc, PAIRS, 0);
   ALLOC(e->strand, PAIRS, 0);
+  e->pair_bytes += e->dev_bytes - b0;
   if (mode == GS_BFS_LEVEL || mode == GS_BFS_BINNED) {
     ALLOC(e->q[0], PAIRS, 0);
     ALLOC(e->q[1], PAIRS, 0);
@@ -280,9 +307,14 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
     ALLOC(e->mv_T, g.rows_cap * g.TW, 0);
     ALLOC(e->mv_area, g.area_cap, 0);
     ALLOC(e->mv_ctr, 4, 0);
-    ALLOC(e->mv_pool, (size_t)g.nbf * g.pcap, 0);
-    ALLOC(e->mv_pused, g.nbf, 0);
-    ALLOC(e->mv_Lt, (size_t)256 * g.nbf, 0);
+    const uint32_t fno = mv_kept_bins(*e);  // a partition rank pools records to its own nodes only
+    e->part_flo = e->vlo >> g.BSF;
+    e->part_fno = fno;
+    b0 = e->dev_bytes;
+    ALLOC(e->mv_pool, (size_t)fno * g.pcap, 0);
+    ALLOC(e->mv_pused, fno, 0);
+    ALLOC(e->mv_Lt, (size_t)256 * fno, 0);
+    e->pair_bytes += e->dev_bytes - b0;
     ALLOC(e->mv_fcls, N, 0xFF);
     ALLOC(e->mv_fk, S, 0);
     ALLOC(e->mv_thr, S, 0);
@@ -300,8 +332,6 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   ALLOC(e->rot_list, N, 0);
   ALLOC(e->rot_count, 2, 0);
   ALLOC(e->rot_changed, N * NB, 0);
-  ALLOC(e->work, PAIRS, 0);
-  ALLOC(e->work_count, 1, 0);
   ALLOC(e->rs_u32, S * 4, 0);
   ALLOC(e->rs_ssum, S, 0);
   ALLOC(e->rs_hist, S * 256, 0);
@@ -313,6 +343,14 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   e->sum_cap = (uint32_t)std::max<size_t>(64, std::min<size_t>(4096, (256ull << 20) / (S * sizeof(gs_round_summary))));
   ALLOC(e->sum, (size_t)e->sum_cap * S, 0);
   ALLOC(e->err, 4, 0);
+  if (e->part_on) {  // prune records of a round (the buffer grows in a prune wave)
+    e->part_rec_cap = std::max<size_t>(1u << 16, PAIRS);
+    const size_t b1 = e->dev_bytes;
+    ALLOC(e->part_rec, e->part_rec_cap, 0);
+    e->pair_bytes += e->dev_bytes - b1;
+    ALLOC(e->part_cnt, 1, 0);
+    ALLOC(e->part_stats, part_stats_words(*e), 0);
+  }
   if (const char* pp = std::getenv("GS_PHASE_PROFILE"); pp && pp[0] == '1') ALLOC(e->phase_clk, 16, 0);
 
   // stakes, buckets and the static rotation prefix sums
@@ -349,6 +387,16 @@ int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t
   if (hipStreamSynchronize(e->st) != hipSuccess) { destroy_engine(e); return fail(GS_EHIP, "create sync"); }
   *out = reinterpret_cast<gs_engine*>(e);
   return GS_OK;
+}
+
+int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t n_slots, gs_engine** out) {
+  return create_engine(prm, stakes, n, n_slots, 0, 1, out);
+}
+
+int gs_create_part(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t n_slots, uint32_t rank,
+                   uint32_t nranks, gs_engine** out) {
+  if (nranks < 1 || rank >= nranks) return fail(GS_EINVAL, "rank must be < nranks");
+  return create_engine(prm, stakes, n, n_slots, rank, nranks, out);
 }
 
 void gs_destroy(gs_engine* eh) { destroy_engine(reinterpret_cast<Engine*>(eh)); }
@@ -510,7 +558,23 @@ static int flush_rot_clear(Engine* e) {
   return GS_OK;
 }
 
+// The step-wise gather's inbound rows [capin][PAIRS]: the multi-source BFS allocates them
+// on first use (its gs_round consumes the records on-chip and never needs them).
+static int ensure_inb(Engine* e) {
+  if (e->inb) return GS_OK;
+  const size_t b0 = e->dev_bytes;
+  const int s = dalloc(*e, &e->inb, (size_t)e->capin * e->PAIRS, 0);
+  e->pair_bytes += e->dev_bytes - b0;
+  return s;
+}
+
+static int refuse_part(Engine* e) {
+  return e->part_on ? fail(GS_ESTATE, "a node-range partition rank runs rounds with gs_part_round") : GS_OK;
+}
+
 static int do_bfs(Engine* e, bool record) {
+  if (int s = refuse_part(e)) return s;
+  if (int s = ensure_inb(e)) return s;
   hipEvent_t t0 = nullptr;
   const bool self_timed = e->bfs_mode == GS_BFS_MULTI;  // times its levels and its gather itself
   if (!self_timed) e->tbegin("bfs", &t0);
@@ -530,6 +594,7 @@ int gs_run_gossip(gs_engine* eh) {
 }
 
 static int do_cp(Engine* e, bool c, bool p, bool a, bool record = false) {
+  if (int s = refuse_part(e)) return s;
   if (int s = flush_rot_clear(e)) return s;
   hipEvent_t t0;
   e->tbegin("consume", &t0);
@@ -578,12 +643,14 @@ static int do_stats(Engine* e, int mode) {
 
 int gs_record_round(gs_engine* eh) {
   ENGINE(eh);
+  if (int s = refuse_part(e)) return s;
   if (int s = need_slots(e)) return s;
   return do_stats(e, 0);
 }
 
 int gs_round(gs_engine* eh, uint32_t round, int record) {
   ENGINE(eh);
+  if (int s = refuse_part(e)) return s;
   if (int s = need_slots(e)) return s;
   const bool rec = record != 0;
   if (e->fused) {  // BFS + consume + prune + statistics in one kernel per slot
@@ -632,7 +699,8 @@ int gs_read_hops(gs_engine* eh, uint32_t slot, uint8_t* hops) {
   ENGINE(eh);
   SLOT_CHECK(slot);
   if (int s = check_err(e)) return s;
-  HIPC(hipMemcpyAsync(hops, e->hops + (size_t)slot * e->N, e->N, hipMemcpyDeviceToHost, e->st));
+  if (e->part_on) std::memset(hops, 0xFF, e->N);  // a partition rank knows its own nodes' hops
+  HIPC(hipMemcpyAsync(hops + e->vlo, e->hops + (size_t)slot * e->NP, e->NP, hipMemcpyDeviceToHost, e->st));
   HIPC(hipStreamSynchronize(e->st));
   return GS_OK;
 }
@@ -667,10 +735,11 @@ int gs_read_inbound(gs_engine* eh, uint32_t slot, uint32_t* off, uint32_t* src, 
 }
 
 // Copies the cache columns of one slot and splits the slot words (ck_make):
-// keys [CACHE_CAP][N] node ids, scores [CACHE_CAP][N] score | PRUNED_FLAG.
+// keys [CACHE_CAP][NP] node ids, scores [CACHE_CAP][NP] score | PRUNED_FLAG (column i =
+// node vlo + i).
 static int read_cache_slot(Engine* e, uint32_t slot, std::vector<uint32_t>& meta, std::vector<uint32_t>& keys,
                            std::vector<uint8_t>& scores) {
-  const size_t N = e->N, base = (size_t)slot * N;
+  const size_t N = e->NP, base = (size_t)slot * N;
   meta.resize(N); keys.resize(N * CACHE_CAP); scores.resize(N * CACHE_CAP);
   HIPC(hipMemcpyAsync(meta.data(), e->cmeta + base, N * 4, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpy2DAsync(keys.data(), N * 4, e->ckey + base, e->PAIRS * 4, N * 4, CACHE_CAP, hipMemcpyDeviceToHost,
@@ -691,11 +760,11 @@ int gs_read_prunes(gs_engine* eh, uint32_t slot, uint32_t* pruner, uint32_t* pru
   std::vector<uint8_t> sc;
   if (int s = read_cache_slot(e, slot, meta, keys, sc)) return s;
   std::vector<std::pair<uint32_t, uint32_t>> pr;
-  const size_t N = e->N;
+  const size_t N = e->NP;  // a partition rank reports its own pruners
   for (size_t v = 0; v < N; ++v) {
     const uint32_t plen = (meta[v] >> 16) & 0xFF;
     for (uint32_t i = 0; i < plen; ++i)
-      if (sc[i * N + v] & PRUNED_FLAG) pr.push_back({(uint32_t)v, keys[i * N + v]});
+      if (sc[i * N + v] & PRUNED_FLAG) pr.push_back({(uint32_t)(e->vlo + v), keys[i * N + v]});
   }
   std::sort(pr.begin(), pr.end());
   *count = pr.size();
@@ -709,8 +778,9 @@ int gs_read_cache(gs_engine* eh, uint32_t slot, uint32_t node, uint32_t* up, uin
   ENGINE(eh);
   SLOT_CHECK(slot);
   if (node >= e->N) return fail(GS_EINVAL, "node out of range");
+  if (node - e->vlo >= e->NP) return fail(GS_EINVAL, "node is not owned by this partition rank");
   if (int s = check_err(e)) return s;
-  const size_t p = (size_t)slot * e->N + node;
+  const size_t p = (size_t)slot * e->NP + (node - e->vlo);
   uint32_t meta = 0;
   uint32_t* dk = nullptr;
   HIPC(hipMalloc(&dk, CACHE_CAP * 4));
@@ -779,18 +849,20 @@ int gs_read_caches(gs_engine* eh, uint32_t slot, uint32_t* up, uint32_t* len, ui
   std::vector<uint32_t> meta, k;
   std::vector<uint8_t> sc;
   if (int s = read_cache_slot(e, slot, meta, k, sc)) return s;
-  const size_t N = e->N;
+  const size_t N = e->NP;
   std::vector<std::pair<uint32_t, uint32_t>> v;
-  for (size_t n = 0; n < N; ++n) {
-    const uint32_t L = meta[n] & 0xFF;
-    up[n] = (meta[n] >> 8) & 0xFF;
-    len[n] = L;
+  for (size_t n0 = 0; n0 < e->N; ++n0) {
+    const size_t n = n0 - e->vlo;  // column of node n0 (a partition rank's own nodes only)
+    const bool own = n < N;
+    const uint32_t L = own ? meta[n] & 0xFF : 0u;
+    up[n0] = own ? (meta[n] >> 8) & 0xFF : 0u;
+    len[n0] = L;
     v.clear();
     for (uint32_t i = 0; i < L; ++i) v.push_back({k[i * N + n], (uint32_t)(sc[i * N + n] & 0x7F)});
     std::sort(v.begin(), v.end());
     for (uint32_t i = 0; i < CACHE_CAP; ++i) {
-      keys[n * CACHE_CAP + i] = i < L ? v[i].first : 0xFFFFFFFFu;
-      scores[n * CACHE_CAP + i] = i < L ? v[i].second : 0;
+      keys[n0 * CACHE_CAP + i] = i < L ? v[i].first : 0xFFFFFFFFu;
+      scores[n0 * CACHE_CAP + i] = i < L ? v[i].second : 0;
     }
   }
   return GS_OK;
@@ -829,7 +901,7 @@ int gs_read_counters(gs_engine* eh, uint32_t slot, uint32_t* egress, uint32_t* i
   ENGINE(eh);
   SLOT_CHECK(slot);
   if (int s = check_err(e)) return s;
-  const size_t N = e->N, base = (size_t)slot * N;
+  const size_t N = e->NP, base = (size_t)slot * N, o = e->vlo;  // a partition rank: its own nodes, 0 elsewhere
   std::vector<uint8_t> eg(N), hp(N), pr(N);
   if (e->esu == 1) {
     HIPC(hipMemcpyAsync(eg.data(), e->egress + slot * e->eso, N, hipMemcpyDeviceToHost, e->st));
@@ -838,11 +910,18 @@ int gs_read_counters(gs_engine* eh, uint32_t slot, uint32_t* egress, uint32_t* i
   }
   HIPC(hipMemcpyAsync(hp.data(), e->hops + base, N, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpyAsync(pr.data(), e->prune_round + base, N, hipMemcpyDeviceToHost, e->st));
-  if (ingress) HIPC(hipMemcpyAsync(ingress, e->cnt + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  if (ingress) {
+    if (e->part_on) std::memset(ingress, 0, (size_t)e->N * 4);
+    HIPC(hipMemcpyAsync(ingress + o, e->cnt + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  }
   HIPC(hipStreamSynchronize(e->st));
+  if (e->part_on) {
+    if (egress) std::memset(egress, 0, (size_t)e->N * 4);
+    if (prune_sent) std::memset(prune_sent, 0, (size_t)e->N * 4);
+  }
   for (size_t v = 0; v < N; ++v) {
-    if (egress) egress[v] = hp[v] != 0xFF ? eg[v] : 0;
-    if (prune_sent) prune_sent[v] = pr[v];
+    if (egress) egress[o + v] = hp[v] != 0xFF ? eg[v] : 0;
+    if (prune_sent) prune_sent[o + v] = pr[v];
   }
   return GS_OK;
 }
@@ -862,18 +941,26 @@ int gs_read_accumulators(gs_engine* eh, uint32_t slot, uint64_t* egress, uint64_
   ENGINE(eh);
   SLOT_CHECK(slot);
   if (int s = check_err(e)) return s;
-  const size_t N = e->N, base = (size_t)slot * N;
+  const size_t N = e->NP, base = (size_t)slot * N, o = e->vlo;  // a partition rank: its own nodes, 0 elsewhere
   std::vector<uint32_t> a(N), b(N), c(N);
   HIPC(hipMemcpyAsync(a.data(), e->egress_acc + base, N * 4, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpyAsync(b.data(), e->ingress_acc + base, N * 4, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpyAsync(c.data(), e->prune_acc + base, N * 4, hipMemcpyDeviceToHost, e->st));
-  if (stranded_times) HIPC(hipMemcpyAsync(stranded_times, e->strand + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  if (stranded_times) {
+    if (e->part_on) std::memset(stranded_times, 0, (size_t)e->N * 4);
+    HIPC(hipMemcpyAsync(stranded_times + o, e->strand + base, N * 4, hipMemcpyDeviceToHost, e->st));
+  }
   if (hop_hist) HIPC(hipMemcpyAsync(hop_hist, e->hist_acc + (size_t)slot * 256, 256 * 8, hipMemcpyDeviceToHost, e->st));
   HIPC(hipStreamSynchronize(e->st));
+  if (e->part_on) {
+    if (egress) std::memset(egress, 0, (size_t)e->N * 8);
+    if (ingress) std::memset(ingress, 0, (size_t)e->N * 8);
+    if (prunes) std::memset(prunes, 0, (size_t)e->N * 8);
+  }
   for (size_t v = 0; v < N; ++v) {
-    if (egress) egress[v] = a[v];
-    if (ingress) ingress[v] = b[v];
-    if (prunes) prunes[v] = c[v];
+    if (egress) egress[o + v] = a[v];
+    if (ingress) ingress[o + v] = b[v];
+    if (prunes) prunes[o + v] = c[v];
   }
   return GS_OK;
 }
@@ -953,6 +1040,13 @@ int gs_engine_info(gs_engine* eh, uint32_t* n_nodes, uint32_t* n_slots, uint32_t
   return GS_OK;
 }
 
+int gs_engine_memory(gs_engine* eh, uint64_t* pair_bytes, uint64_t* other_bytes) {
+  ENGINE(eh);
+  if (pair_bytes) *pair_bytes = e->pair_bytes;
+  if (other_bytes) *other_bytes = e->dev_bytes - e->pair_bytes;
+  return GS_OK;
+}
+
 // ----------------------------------------------------------------- MST ----
 // Cluster::mst (gossip.rs:580-591): the first discoverer of every reached node in the
 // reference's FIFO queue order. The queue is level by level; within a level, nodes are
@@ -967,6 +1061,7 @@ int gs_read_mst(gs_engine* eh, uint32_t slot, uint32_t* parent) {
   if (!e->inb_valid)
     return fail(GS_ESTATE, "inbound records are kept on-chip by gs_round (the one-kernel round, or the "
                            "multi-source BFS's fused gather + consume); call gs_run_gossip to materialize them");
+  if (int s = refuse_part(e)) return s;
   if (e->N > (1u << 18)) return fail(GS_ERANGE, "gs_read_mst is a debug readback for n <= 262,144");
   const uint32_t N = e->N, org = e->slots[slot].origin;
   std::vector<uint8_t> hops(N);
@@ -1023,107 +1118,91 @@ int gs_read_mst(gs_engine* eh, uint32_t slot, uint32_t* parent) {
 // ---------------------------------------------------- node-range partition ----
 #define PART(eh)                                                            \
   ENGINE(eh);                                                               \
-  if (!e->part_on) return fail(GS_ESTATE, "gs_part_attach has not been called");
+  if (!e->part_on) return fail(GS_ESTATE, "not a node-range partition rank (gs_create_part)");
 
 static hipMemcpyKind kind_to(int dev) { return dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost; }
 static hipMemcpyKind kind_from(int dev) { return dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice; }
 
-int gs_part_attach(gs_engine* eh, uint32_t rank, uint32_t nranks) {
-  ENGINE(eh);
-  if (nranks < 1 || rank >= nranks) return fail(GS_EINVAL, "rank must be < nranks");
-  if (e->bfs_mode != GS_BFS_LEVEL) return fail(GS_EINVAL, "a node-range partition needs bfs_mode GS_BFS_LEVEL");
-  if (e->part_on) return fail(GS_ESTATE, "already attached");
-  e->part_K = nranks;
-  e->part_rank = rank;
-  e->part_C = (e->N + nranks - 1) / nranks;
-  e->part_lo = std::min(e->N, rank * e->part_C);
-  e->part_hi = std::min(e->N, e->part_lo + e->part_C);
-  e->part_Wr = (e->part_C + 31) / 32;
-  ALLOC(e->part_fr_all, (size_t)nranks * e->S * e->part_Wr, 0);
-  ALLOC(e->part_fr_own, (size_t)e->S * e->part_Wr, 0);
-  ALLOC(e->part_delta, e->PAIRS, 0);
-  ALLOC(e->part_cnt, 2, 0);
-  ALLOC(e->part_stats, part_stats_words(*e), 0);
-  e->part_on = true;
-  return GS_OK;
-}
-
-int gs_part_sizes(gs_engine* eh, size_t* fw, size_t* dw, size_t* sw, uint32_t* lo, uint32_t* hi) {
+int gs_part_sizes(gs_engine* eh, size_t* stats_words, uint32_t* lo, uint32_t* hi) {
   PART(eh);
-  if (fw) *fw = (size_t)e->S * e->part_Wr;
-  if (dw) *dw = e->PAIRS;
-  if (sw) *sw = part_stats_words(*e);
+  if (stats_words) *stats_words = part_stats_words(*e);
   if (lo) *lo = e->part_lo;
   if (hi) *hi = e->part_hi;
   return GS_OK;
 }
 
-int gs_part_begin(gs_engine* eh) {
+int gs_part_round(gs_engine* eh, uint32_t round, int record, uint32_t* n_records) {
   PART(eh);
+  if (!n_records) return fail(GS_EINVAL, "null argument");
   if (int s = need_slots(e)) return s;
+  if (round >= (1u << 27)) return fail(GS_ERANGE, "round index must be < 2^27");
   if (int s = flush_rot_clear(e)) return s;
-  HIPC(launch_part_begin(*e));
-  return GS_OK;
-}
-
-int gs_part_level(gs_engine* eh, uint32_t level, uint32_t* new_local) {
-  PART(eh);
-  if (!new_local) return fail(GS_EINVAL, "null argument");
-  if (level + 1 >= 255) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
-  HIPC(launch_part_level(*e, level));
-  HIPC(hipMemcpyAsync(e->h_err + 1, e->part_cnt + 1, 4, hipMemcpyDeviceToHost, e->st));
+  const bool rec = record != 0;
+  HIPC(hipMemsetAsync(e->part_cnt, 0, 4, e->st));
+  hipError_t r = launch_bfs_multi(*e, rec, true);  // the whole BFS; gather + consume of own nodes
+  e->inb_valid = false;
+  if (r == hipErrorNotSupported) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
+  HIPC(r);
+  hipEvent_t t0;
+  e->tbegin("consume", &t0);
+  r = hipMemsetAsync(e->slot_prunes, 0, e->S * 4, e->st);
+  if (r == hipSuccess) r = launch_consume_prune_g(*e, rec, false);  // send_prunes of own pruners
+  if (r == hipSuccess) r = launch_part_emit(*e);                    // ... as records for the other ranks
+  e->tend("consume", t0);
+  HIPC(r);
+  HIPC(hipMemcpyAsync(e->h_err + 1, e->part_cnt, 4, hipMemcpyDeviceToHost, e->st));
   HIPC(hipStreamSynchronize(e->st));
-  *new_local = e->h_err[1];
-  e->inb_valid = true;
+  if (int s = check_err(e)) return s;
+  if (e->h_err[1] > e->part_rec_cap) {  // a prune wave: grow the record buffer and emit again
+    const size_t cap = (size_t)e->h_err[1] + e->h_err[1] / 4;
+    uint2* nb = nullptr;
+    HIPC(hipMalloc(&nb, cap * 8));
+    for (auto& p : e->allocs)
+      if (p == e->part_rec) { hipFree(p); p = nb; }
+    e->pair_bytes += (cap - e->part_rec_cap) * 8;
+    e->dev_bytes += (cap - e->part_rec_cap) * 8;
+    e->part_rec = nb;
+    e->part_rec_cap = cap;
+    HIPC(hipMemsetAsync(e->part_cnt, 0, 4, e->st));
+    HIPC(launch_part_emit(*e));
+    HIPC(hipMemcpyAsync(e->h_err + 1, e->part_cnt, 4, hipMemcpyDeviceToHost, e->st));
+    HIPC(hipStreamSynchronize(e->st));
+  }
+  e->part_nrec = e->h_err[1];
+  *n_records = e->part_nrec;
   return GS_OK;
 }
 
-int gs_part_frontier_out(gs_engine* eh, void* dst, int dev) {
+int gs_part_prunes_out(gs_engine* eh, void* dst, int dev) {
   PART(eh);
-  HIPC(hipMemcpyAsync(dst, e->part_fr_own, (size_t)e->S * e->part_Wr * 4, kind_to(dev), e->st));
-  HIPC(hipStreamSynchronize(e->st));
-  return GS_OK;
-}
-
-int gs_part_frontier_in(gs_engine* eh, const void* src, int dev) {
-  PART(eh);
-  HIPC(hipMemcpyAsync(e->part_fr_all, src, (size_t)e->part_K * e->S * e->part_Wr * 4, kind_from(dev), e->st));
-  HIPC(hipStreamSynchronize(e->st));
-  return GS_OK;
-}
-
-int gs_part_consume(gs_engine* eh, uint32_t* local_prunes) {
-  PART(eh);
-  if (!local_prunes) return fail(GS_EINVAL, "null argument");
-  HIPC(hipMemsetAsync(e->part_delta, 0, e->PAIRS * 4, e->st));
-  HIPC(launch_consume_prune(*e, true, true, true, false));  // accumulators: gs_part_stats_out
-  std::vector<uint32_t> sp(e->S);
-  HIPC(hipMemcpyAsync(sp.data(), e->slot_prunes, e->S * 4, hipMemcpyDeviceToHost, e->st));
-  HIPC(hipStreamSynchronize(e->st));
-  uint64_t t = 0;
-  for (uint32_t x : sp) t += x;
-  *local_prunes = (uint32_t)std::min<uint64_t>(t, 0xFFFFFFFFu);
-  return GS_OK;
-}
-
-int gs_part_delta_out(gs_engine* eh, void* dst, int dev) {
-  PART(eh);
-  HIPC(hipMemcpyAsync(dst, e->part_delta, e->PAIRS * 4, kind_to(dev), e->st));
+  if (e->part_nrec) HIPC(hipMemcpyAsync(dst, e->part_rec, (size_t)e->part_nrec * 8, kind_to(dev), e->st));
   HIPC(hipStreamSynchronize(e->st));
   return GS_OK;
 }
 
-int gs_part_delta_in(gs_engine* eh, const void* src, int dev) {
+int gs_part_prunes_in(gs_engine* eh, const void* src, size_t n, int dev) {
   PART(eh);
-  HIPC(hipMemcpyAsync(e->part_delta, src, e->PAIRS * 4, kind_from(dev), e->st));
-  HIPC(launch_part_delta_apply(*e));
+  if (n == 0) return GS_OK;
+  const uint2* rec = reinterpret_cast<const uint2*>(src);
+  if (!dev) {  // host records: staged in a grow-only device buffer
+    if (n > e->part_in_cap) {
+      if (e->part_in) hipFree(e->part_in);
+      e->part_in = nullptr;
+      e->part_in_cap = 0;
+      HIPC(hipMalloc(&e->part_in, n * 8));
+      e->part_in_cap = n;
+    }
+    HIPC(hipMemcpyAsync(e->part_in, src, n * 8, hipMemcpyHostToDevice, e->st));
+    rec = e->part_in;
+  }
+  HIPC(launch_part_prunes_apply(*e, rec, n));
   HIPC(hipStreamSynchronize(e->st));
-  return GS_OK;
+  return check_err(e);
 }
 
 int gs_part_stats_out(gs_engine* eh, void* dst, int dev) {
   PART(eh);
-  HIPC(launch_stats(*e, e->sum_used, 3));  // this rank's nodes: partials (and its accumulators)
+  HIPC(launch_stats(*e, e->sum_used, 5));  // this rank's nodes: partials (and its egress accumulators)
   HIPC(launch_part_stats_pack(*e));
   HIPC(hipMemcpyAsync(dst, e->part_stats, part_stats_words(*e) * 8, kind_to(dev), e->st));
   HIPC(hipStreamSynchronize(e->st));

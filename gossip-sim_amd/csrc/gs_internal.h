@@ -14,7 +14,8 @@ namespace gs {
 //  per node      stake u64, bucket u8, fail rank u32, stake rank u32
 //  per (node,k)  peers[ASZP] u32 ring + hl u16 (head | len << 8)      -- PushActiveSet
 //  per k         prefix sums of rotation weights P[k][N+1] u64
-//  per pair      (slot-major pair p = slot * N + node)
+//  per pair      (slot-major pair p = slot * NP + (node - vlo): NP = N, vlo = 0, except
+//                on a node-range partition rank, which keeps its own nodes [vlo, vlo + NP))
 //                hops u8, in-degree u32, prune mask u32 (bits = physical ring slots),
 //                inbound records u32 [capin][pairs] (hop << 24 | src),
 //                cache meta u32 (len | upserts << 8 | pruned-len << 16),
@@ -40,7 +41,8 @@ struct MvGroup { uint32_t s0, sg, seed0, nseed; };
 struct Engine {
   gs_params prm{};
   uint32_t N = 0, S = 0;
-  size_t PAIRS = 0;
+  uint32_t NP = 0, vlo = 0;  // nodes with per-pair state: [vlo, vlo + NP) (all N but on a partition rank)
+  size_t PAIRS = 0;          // S * NP
   uint32_t ASZ = 0, ASZP = 0, fanout = 0, capin = 64;
   uint32_t bfs_mode = GS_BFS_LEVEL;
   uint32_t fcap = 0;             // min(fanout, active_set_size): pushes per node
@@ -53,6 +55,7 @@ struct Engine {
   bool inb_valid = true;         // inbound records materialized in HBM (step-wise BFS)
   hipStream_t st = nullptr;
   size_t dev_bytes = 0;
+  size_t pair_bytes = 0;  // of which per-(slot, node) state (gs_engine_memory)
   std::vector<void*> allocs;
 
   // node arrays
@@ -120,7 +123,6 @@ struct Engine {
   uint32_t* mv_gtab = nullptr;    // [groups][GT_WORDS]
   uint2* mv_seed = nullptr;       // [S] seed entries (distinct origins) of every group
   std::vector<MvGroup> mv_groups;
-  hipEvent_t mv_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool mv_attr_set = false;
   bool mv_diag = false;  // GS_MV_DIAG=1
   bool mv_fused = true;  // gs_round: fused gather + consume (GS_MV_FUSED=0: gather, then k_cg_consume)
@@ -134,16 +136,16 @@ struct Engine {
   uint32_t rot_parity = 0;          // parity of the last rotation's round
   size_t rwg_attr_lds = 0;          // dynamic LDS the round kernel was last configured for
   // node-range partition (gs_partition.hip): this rank owns node ids [part_lo, part_hi)
+  // (= [vlo, vlo + NP)) and the fine bins [part_flo, part_flo + part_fno) of the multi BFS
   bool part_on = false;
-  uint32_t part_rank = 0, part_K = 1, part_lo = 0, part_hi = 0, part_C = 0, part_Wr = 0;
-  uint32_t* part_fr_all = nullptr;  // global frontier bitsets [K][S][Wr]
-  uint32_t* part_fr_own = nullptr;  // this rank's next-level bits [S][Wr]
-  uint32_t* part_delta = nullptr;   // prune-mask bits set this round [S][N] (summed over ranks = OR)
-  uint32_t* part_cnt = nullptr;     // [2]: frontier queue length, new local nodes
+  uint32_t part_rank = 0, part_K = 1, part_lo = 0, part_hi = 0, part_flo = 0, part_fno = 0;
+  uint2* part_rec = nullptr;        // prune records of this rank's round: (slot * N + prunee, ring bits), grow-only
+  size_t part_rec_cap = 0;
+  uint32_t* part_cnt = nullptr;     // [1]: prune records staged
+  uint32_t part_nrec = 0;           // records of the last gs_part_round
+  uint2* part_in = nullptr;         // every rank's prune records (gs_part_prunes_in), grow-only
+  size_t part_in_cap = 0;
   uint64_t* part_stats = nullptr;   // packed stats partials [S][5 + 256 + bm_words]
-  // fused consume -> prune worklist
-  uint32_t* work = nullptr;
-  uint32_t* work_count = nullptr;
   // stats
   uint32_t* rs_u32 = nullptr;   // per slot: visited, pushes, stranded, pad
   uint64_t* rs_ssum = nullptr;  // per slot: stranded stake sum
@@ -196,6 +198,7 @@ void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g, bool allo
 bool bin_supported(const BinGeom& g, uint32_t fcap);
 void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g);
 bool mv_supported(const MvGeom& g, uint32_t ASZP);
+uint32_t mv_kept_bins(const Engine& e);
 void mv_build_groups(Engine& e, const std::vector<uint32_t>& origins, const std::vector<uint8_t>& obkt,
                      const std::vector<uint8_t>& bucket, std::vector<uint32_t>& gtab, std::vector<uint2>& seeds);
 // consume: gs_round's fused gather + consume (k_mv_consume) instead of the materializing
@@ -208,11 +211,10 @@ hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply,
 hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume = true);
 // node-range partition (gs_partition.hip)
 size_t part_stats_words(const Engine& e);
-hipError_t launch_part_begin(Engine& e);
-hipError_t launch_part_level(Engine& e, uint32_t level);
 hipError_t launch_part_stats_pack(Engine& e);
 hipError_t launch_part_stats_unpack(Engine& e);
-hipError_t launch_part_delta_apply(Engine& e);
+hipError_t launch_part_prunes_apply(Engine& e, const uint2* rec, size_t n);
+hipError_t launch_part_emit(Engine& e);  // this round's prune records -> part_rec (count in part_cnt)
 // Rotation of round `round` (decide + entries); the prune-bit clear of the replaced
 // ring slots runs now, or with defer_clear it is left pending for the next one-kernel
 // round (which applies it to its LDS copy of the masks) or launch_rotate_clear.

@@ -715,102 +715,6 @@ __device__ inline void cp_generic(const CpArgs& a, size_t p, uint32_t o, uint32_
   a.cmeta[p] = meta;
 }
 
-// Fused fast path (in-degree <= 16, cache length + in-degree <= 24, the steady
-// state): inbound records sorted in registers by a sorting network, the cache
-// entry held in registers, only changed slots written back.
-constexpr int FC = 16, FL = 16;
-
-__device__ inline void cp_fast(const CpArgs& a, size_t p, uint32_t c, uint32_t meta) {
-  const size_t PAIRS = a.PAIRS;
-  uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
-  if (c == 0) {  // nothing received: only the pruned-len field resets
-    if (meta & 0xFF0000u) a.cmeta[p] = meta & 0xFFFFu;
-    return;
-  }
-  // Row bases (i * PAIRS) are wave-uniform (scalar registers); the lane offset is a
-  // 32-bit pair index. Loads are bounded by the wave's maximum length (a uniform
-  // branch) and issued unconditionally, then masked: no per-load waits.
-  const uint32_t q = (uint32_t)p;
-  const uint32_t wlen = active_max_small(len);
-  uint32_t key[FL], sc[FL];
-#pragma unroll
-  for (int i = 0; i < FL; ++i) {
-    key[i] = 0xFFFFFFFFu;
-    sc[i] = 0;
-    if ((uint32_t)i < wlen) {
-      const uint32_t w = (a.ckey + (size_t)i * PAIRS)[q];
-      key[i] = ck_id(w);
-      sc[i] = ck_score(w);
-    }
-  }
-  asm volatile("" ::: "memory");  // keep the loads above: one wait for all of them
-#ifdef GS_DEBUG_BOUNDS
-  for (int i = 0; i < FL; ++i)
-    if ((uint32_t)i < len && GS_OOB(key[i], a.N, a.err, "cp_fast cached key")) return;
-  if (GS_OOB(p, PAIRS, a.err, "cp_fast p")) return;
-#endif
-#pragma unroll
-  for (int i = 0; i < FL; ++i) {
-    const bool in = (uint32_t)i < len;
-    key[i] = in ? key[i] : 0xFFFFFFFFu;
-    sc[i] = in ? sc[i] : 0u;  // live entries never carry the pruned flag (set only as len resets)
-  }
-  uint32_t dirty = 0;
-  if (c) {
-    uint32_t r[FC];
-    const uint32_t wc = active_max_small(c);
-#pragma unroll
-    for (int j = 0; j < FC; ++j) {
-      r[j] = 0xFFFFFFFFu;
-      if ((uint32_t)j < wc) r[j] = (a.inb + (size_t)j * PAIRS)[q];
-    }
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < FC; ++j) r[j] = (uint32_t)j < c ? r[j] : 0xFFFFFFFFu;
-#ifdef GS_DEBUG_BOUNDS
-    for (int j = 0; j < FC; ++j)
-      if ((uint32_t)j < c && GS_OOB(r[j] & 0xFFFFFFu, a.N, a.err, "cp_fast record src")) return;
-#endif
-    sort16(r);
-    up = up < 255 ? up + 1 : 255;  // rank 0 (received_cache.rs:84-86)
-#pragma unroll
-    for (int k = 0; k < FC; ++k) {
-      if ((uint32_t)k >= c) break;
-      const uint32_t src = r[k] & 0xFFFFFFu;
-      uint32_t fm = 0;
-#pragma unroll
-      for (int i = 0; i < FL; ++i) fm |= (uint32_t)(key[i] == src) << i;
-      if (k < 2) {  // timely: score += 1, inserted regardless of the 50-key cap
-        if (fm) {
-#pragma unroll
-          for (int i = 0; i < FL; ++i)
-            if ((fm >> i) & 1u) sc[i] = sc[i] < 0x7F ? sc[i] + 1 : 0x7F;
-          dirty |= fm;
-        } else {
-#pragma unroll
-          for (int i = 0; i < FL; ++i)
-            if ((uint32_t)i == len) { key[i] = src; sc[i] = 1; }
-          dirty |= 1u << len;
-          ++len;
-        }
-      } else if (!fm && len < CACHE_LIMIT) {
-#pragma unroll
-        for (int i = 0; i < FL; ++i)
-          if ((uint32_t)i == len) { key[i] = src; sc[i] = 0; }
-        dirty |= 1u << len;
-        ++len;
-      }
-    }
-    if (a.record) a.ingress_acc[p] += c;
-  }
-#pragma unroll
-  for (int i = 0; i < FL; ++i)
-    if ((dirty >> i) & 1u) {
-      (a.ckey + (size_t)i * PAIRS)[q] = ck_make(key[i], sc[i]);
-    }
-  a.cmeta[p] = len | (up << 8);
-}
-
 // Step-wise forms (gs_consume_messages / gs_send_prunes / gs_prune_connections).
 template <bool CONSUME, bool PRUNE, bool APPLY>
 __global__ __launch_bounds__(256) void k_consume_prune(CpArgs a) {
@@ -821,53 +725,6 @@ __global__ __launch_bounds__(256) void k_consume_prune(CpArgs a) {
     cp_generic<CONSUME, PRUNE, APPLY>(a, p, o, v, cache_overflow);
   }
   if (cache_overflow) atomicOr(a.err, ERR_CACHE);
-}
-
-// Fused round, kernel 1: consume every pair (register fast path when the inbound
-// list and the cache entry fit), then queue the pairs whose prune is due.
-__global__ __launch_bounds__(256) void k_consume_fused(CpArgs a, uint32_t* __restrict__ work,
-                                                       uint32_t* __restrict__ work_count) {
-  bool cache_overflow = false;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.PAIRS; p += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t meta = a.cmeta[p];
-    uint32_t c = a.cnt[p];
-    if (c > a.capin) c = a.capin;
-    if (c <= (uint32_t)FC && (meta & 0xFF) + c <= (uint32_t)FL) {
-      cp_fast(a, p, c, meta);
-    } else {
-      const uint32_t o = (uint32_t)(p / a.N);
-      cp_generic<true, false, false>(a, p, o, (uint32_t)(p - (size_t)o * a.N), cache_overflow);
-    }
-    const uint32_t m2 = a.cmeta[p];
-    const bool due = ((m2 >> 8) & 0xFF) >= MIN_NUM_UPSERTS;
-    if (!due) {  // send_prunes yields nothing for this pair this round
-      a.prune_round[p] = 0;
-      if (m2 & 0xFF0000u) a.cmeta[p] = m2 & 0xFFFFu;
-    }
-    const unsigned long long bal = __ballot(due);
-    if (bal) {
-      const int leader = __ffsll((long long)bal) - 1;
-      uint32_t base = 0;
-      if ((int)lane_id() == leader) base = atomicAdd(work_count, (uint32_t)__popcll(bal));
-      base = __shfl(base, leader);
-      if (due) work[base + __popcll(bal & ((1ull << lane_id()) - 1))] = (uint32_t)p;
-    }
-  }
-  if (cache_overflow) atomicOr(a.err, ERR_CACHE);
-}
-
-// Fused round, kernel 2: send_prunes + prune_connections for the queued pairs only.
-__global__ __launch_bounds__(256) void k_prune_fused(CpArgs a, const uint32_t* __restrict__ work,
-                                                     const uint32_t* __restrict__ work_count) {
-  bool cache_overflow = false;
-  const uint32_t n = *work_count;
-  if (GS_OOB(n, a.PAIRS + 1, a.err, "prune work count")) return;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const size_t p = work[i];
-    if (GS_OOB(p, a.PAIRS, a.err, "prune work pair")) continue;
-    const uint32_t o = (uint32_t)(p / a.N);
-    cp_generic<false, true, true>(a, p, o, (uint32_t)(p - (size_t)o * a.N), cache_overflow);
-  }
 }
 
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record) {
@@ -914,8 +771,9 @@ struct StatsArgs {
   uint32_t* bm;
   gs_round_summary* sum;
   uint32_t N, S, W;
-  uint32_t lo, hi;
-  size_t eso, esu;  // egress strides of (slot, node)  // nodes of this pass (a node-range partition passes its own range)
+  uint32_t lo, hi;  // nodes of this pass (a node-range partition passes its own range)
+  uint32_t NP, vlo; // pair p = slot * NP + (node - vlo); egress at slot * eso + (node - vlo) * esu
+  size_t eso, esu;  // egress strides of (slot, node)
 };
 
 // FULL: the step-wise gs_record_round (reads the per-round counters of every pair);
@@ -924,7 +782,7 @@ struct StatsArgs {
 template <bool FULL, bool EG = false>
 __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
   const uint32_t o = blockIdx.y;
-  const size_t base = (size_t)o * a.N;
+  const size_t base = (size_t)o * a.NP - a.vlo;
   const uint32_t nf = a.nfail[o];
   __shared__ uint32_t h[256];
   __shared__ uint32_t acc[3];
@@ -947,7 +805,7 @@ __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
     if (hh != 0xFF) {
       ++vis;
       atomicAdd(&h[hh], 1u);
-      if (FULL || EG) a.egress_acc[p] += a.egress[o * a.eso + v * a.esu];
+      if (FULL || EG) a.egress_acc[p] += a.egress[o * a.eso + (v - a.vlo) * a.esu];
     } else if (!(nf && a.frank[v] < nf)) {
       a.strand[p] += 1;
       ++sc;
@@ -1058,8 +916,9 @@ __global__ __launch_bounds__(1024) void k_stats_finalize(StatsArgs a, uint32_t r
 }
 
 // mode 0: full pass; 1: hop-only pass (fused level-synchronous round); 2: finalize only
-// (the workgroup BFS already reduced the round); 3: the full pass only (partition
-// partials); 4: hop pass that also accumulates egress (multi-source BFS round).
+// (the workgroup BFS already reduced the round, or a partition summed its partials);
+// 3: the full pass only; 4: hop pass that also accumulates egress (multi-source BFS
+// round); 5: mode 4's pass only (a partition rank's partials).
 hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   StatsArgs a;
   a.stake = e.stake; a.frank = e.frank; a.srank = e.srank; a.by_srank = e.by_srank; a.nfail = e.nfail;
@@ -1067,13 +926,14 @@ hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   a.egress_acc = e.egress_acc; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc; a.strand = e.strand;
   a.rs_u32 = e.rs_u32; a.rs_ssum = e.rs_ssum; a.rs_hist = e.rs_hist; a.hist_acc = e.hist_acc; a.bm = e.bm;
   a.sum = e.sum; a.N = e.N; a.S = e.S; a.W = e.bm_words; a.eso = e.eso; a.esu = e.esu;
-  a.lo = e.part_on ? e.part_lo : 0u;
-  a.hi = e.part_on ? e.part_hi : e.N;
-  uint32_t gx = grid_for(e.N, 256, std::max<uint32_t>(64, 2048 / std::max<uint32_t>(e.S, 1)));
+  a.lo = e.vlo;
+  a.hi = e.vlo + e.NP;
+  a.NP = e.NP; a.vlo = e.vlo;
+  uint32_t gx = grid_for(e.NP, 256, std::max<uint32_t>(64, 2048 / std::max<uint32_t>(e.S, 1)));
   if (mode == 0 || mode == 3) hipLaunchKernelGGL(k_stats_pass<true>, dim3(gx, e.S), dim3(256), 0, e.st, a);
   else if (mode == 1) hipLaunchKernelGGL(k_stats_pass<false>, dim3(gx, e.S), dim3(256), 0, e.st, a);
-  else if (mode == 4) hipLaunchKernelGGL((k_stats_pass<false, true>), dim3(gx, e.S), dim3(256), 0, e.st, a);
-  if (mode != 3)  // mode 3: the pass only (a partition sums the partials over ranks first)
+  else if (mode == 4 || mode == 5) hipLaunchKernelGGL((k_stats_pass<false, true>), dim3(gx, e.S), dim3(256), 0, e.st, a);
+  if (mode != 3 && mode != 5)  // the pass only (a partition sums the partials over ranks first)
     hipLaunchKernelGGL(k_stats_finalize, dim3(e.S), dim3(1024), 0, e.st, a, rec_slot);
   return hipGetLastError();
 }

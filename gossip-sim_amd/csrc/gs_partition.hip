@@ -1,122 +1,30 @@
 // gs_partition.hip -- node-range partition of one simulation batch over K ranks
 // (per-origin state larger than one GPU).
 //
-// Rank r owns node ids [r*C, min((r+1)*C, N)). Active sets, prune masks and failed
-// flags are replicated: every rank applies the same rotation (Philox), the same failures
-// and the same (exchanged) prune bits. Per BFS level (Cluster::run_gossip,
-// gossip.rs:494-615) every rank expands the WHOLE frontier -- rows and masks are local
-// copies -- but keeps only the pushes whose destination it owns: in-degree, inbound
-// record, first-visit hop and the next-level frontier bit. The frontier of the next level
-// is the all-gather of the ranks' bitsets [K][S][Wr]. consume / send_prunes run on owned
-// destinations; the prune bits they set (prune_connections, gossip.rs:701-737) go to a
-// per-round delta whose sum over ranks is an OR -- a bit belongs to one pruner, owned by
-// one rank -- and is OR-ed into every rank's masks. Statistics are partial sums over owned
-// nodes (counts, hop bins, the stranded bitmap over stake rank), summed over ranks before
-// the per-slot summary is finalized. The exchanges are the caller's (RCCL on device
-// buffers, or host buffers): see include/gossip_hip.h gs_part_*.
+// Rank r owns node ids [lo, hi) (contiguous, starting on a 1,024-node bin). Replicated
+// on every rank: stakes, active-set rows, prune masks and failed flags -- every rank
+// applies the same rotations (Philox), the same failures and the same prune bits.
+// Partitioned: every per-(slot, node) array -- hop counts, in-degrees, received caches,
+// round counters, accumulators, stranded counts -- exists for owned nodes only
+// (S x (hi - lo) pairs), and so do the BFS's per-destination record pools.
+//
+// A round: each rank runs the whole multi-source BFS (Cluster::run_gossip,
+// gossip.rs:494-615) over its replicated rows and masks -- no exchange per level --
+// keeping only the records of pushes to its own nodes; gathers and consumes them
+// (gossip.rs:618-653) and runs send_prunes for its own pruners (gossip.rs:657-699).
+// prune_connections (gossip.rs:701-737) sets bits in the PRUNEE's replicated mask row:
+// each rank stages its prunes as records (slot * N + prunee, ring-slot bits), the
+// ranks all-gather them and every rank ORs every record into its masks. Recorded
+// statistics are partial sums over owned nodes (counts, hop bins, the stranded bitmap
+// over stake rank), summed over ranks before the per-slot summary is finalized. The
+// exchanges are the caller's (RCCL on device buffers, or host buffers): see
+// include/gossip_hip.h gs_part_*.
 #include "gs_device.h"
 #include "gs_internal.h"
 
 namespace gs {
 
 namespace {
-
-// Level 0: the origins, known to every rank.
-__global__ void k_part_seed(uint32_t* fr_all, const uint32_t* __restrict__ origin, uint32_t S, uint32_t Wr,
-                            uint32_t C, uint32_t N, uint32_t lo, uint32_t hi, uint8_t* hops) {
-  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= S) return;
-  const uint32_t u = origin[o], r = u / C, off = u - r * C;
-  atomicOr(&fr_all[((size_t)r * S + o) * Wr + (off >> 5)], 1u << (off & 31));
-  if (u >= lo && u < hi) hops[(size_t)o * N + u] = 0;
-}
-
-// Global frontier bitsets -> queue of pairs (o * N + u); one atomic per wave.
-__global__ __launch_bounds__(256) void k_part_compact(const uint32_t* __restrict__ fr_all, uint32_t K, uint32_t S,
-                                                      uint32_t Wr, uint32_t C, uint32_t N, uint32_t* q,
-                                                      uint32_t* qcount) {
-  const size_t total = (size_t)K * S * Wr;
-  for (size_t i0 = (size_t)blockIdx.x * blockDim.x; i0 < total; i0 += (size_t)gridDim.x * blockDim.x) {
-    const size_t i = i0 + threadIdx.x;
-    const uint32_t w = i < total ? fr_all[i] : 0u;
-    const uint32_t k = __popc(w);
-    const uint32_t incl = wave_incl_scan(k);
-    const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
-    if (!tot) continue;
-    uint32_t b = 0;
-    if (lane_id() == 63) b = atomicAdd(qcount, tot);
-    b = (uint32_t)__shfl((int)b, 63) + incl - k;
-    if (!w) continue;
-    const uint32_t wi = (uint32_t)(i % Wr), ro = (uint32_t)(i / Wr);
-    const uint32_t o = ro % S, r = ro / S;
-    uint32_t m = w;
-    while (m) {
-      const uint32_t bit = __ffs(m) - 1;
-      m &= m - 1;
-      const uint32_t u = r * C + wi * 32 + bit;
-      q[b++] = o * N + u;
-    }
-  }
-}
-
-// One BFS level over the whole frontier, keeping owned destinations.
-template <int ASZP>
-__global__ __launch_bounds__(256) void k_part_expand(
-    const uint32_t* __restrict__ q, const uint32_t* __restrict__ qcount, uint32_t d, const uint8_t* __restrict__ bucket,
-    const uint32_t* __restrict__ peers, const uint16_t* __restrict__ hl, const uint32_t* __restrict__ frank,
-    const uint32_t* __restrict__ origin, const uint8_t* __restrict__ obkt, const uint32_t* __restrict__ nfail,
-    const uint32_t* __restrict__ mask, uint8_t* hops, uint32_t* cnt, uint32_t* inb, uint8_t* egress,
-    uint32_t* fr_own, uint32_t* newcount, uint32_t* err, uint32_t N, uint32_t ASZ, uint32_t fanout, uint32_t capin,
-    size_t PAIRS, uint32_t lo, uint32_t hi, uint32_t Wr) {
-  const uint32_t qn = *qcount;
-  bool overflow = false;
-  for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < qn; i0 += gridDim.x * blockDim.x) {
-    const uint32_t i = i0 + threadIdx.x;
-    const bool valid = i < qn;
-    const uint32_t p = valid ? q[i] : 0u;
-    const uint32_t o = p / N, u = p - o * N;
-    uint32_t fresh = 0;
-    if (valid) {
-      const uint32_t org = origin[o], nf = nfail[o];
-      const uint32_t ent = u * NB + min((uint32_t)bucket[u], (uint32_t)obkt[o]);
-      const uint32_t hv = hl[ent];
-      uint32_t row[ASZP];
-      load_row<ASZP>(peers + (size_t)ent * ASZP, row);
-      // PushActiveSet::get_nodes(..).take(fanout), failed peers burn their slot (gossip.rs:527-541)
-      uint32_t pushm = taken_slots<ASZP>(row, hv & 0xFF, hv >> 8, ASZ, mask[p], org, fanout);
-      if (nf) {
-#pragma unroll
-        for (int s = 0; s < ASZP; ++s)
-          if (((pushm >> s) & 1u) && frank[row[s]] < nf) pushm &= ~(1u << s);
-      }
-      if (u >= lo && u < hi) egress[p] = (uint8_t)__popc(pushm);
-      const size_t base = (size_t)o * N;
-      const uint32_t rec = ((d + 1) << 24) | u;
-      uint32_t old[ASZP];
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) {
-        const bool mine = ((pushm >> s) & 1u) && row[s] >= lo && row[s] < hi;
-        old[s] = mine ? atomicAdd(&cnt[base + row[s]], 1u) : 0xFFFFFFFFu;
-      }
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) {
-        if (old[s] == 0xFFFFFFFFu) continue;
-        const uint32_t w = row[s];
-        if (old[s] < capin) inb[(size_t)old[s] * PAIRS + base + w] = rec;
-        else overflow = true;
-        if (old[s] == 0) {  // first arrival: dist = dist[src] + 1 (gossip.rs:594-600)
-          hops[base + w] = (uint8_t)(d + 1);
-          const uint32_t off = w - lo;
-          atomicOr(&fr_own[(size_t)o * Wr + (off >> 5)], 1u << (off & 31));
-          ++fresh;
-        }
-      }
-    }
-    const uint32_t incl = wave_incl_scan(fresh);
-    if (lane_id() == 63 && incl) atomicAdd(newcount, incl);
-  }
-  if (overflow) atomicOr(err, ERR_INBOUND);
-}
 
 // Stats partials of one slot: visited, pushes, stranded, prunes, stranded stake sum,
 // 256 hop bins, the stranded bitmap (W words), as u64 words.
@@ -152,9 +60,58 @@ __global__ void k_part_stats_unpack(uint32_t S, uint32_t W, const uint64_t* in, 
   }
 }
 
-__global__ void k_part_delta_apply(uint32_t* mask, const uint32_t* __restrict__ delta, size_t n) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    if (delta[i]) mask[i] |= delta[i];
+// PushActiveSet::prune of every rank's prunes (push_active_set.rs:56-71): the record's
+// ring-slot bits OR-ed into the prunee's mask word of the slot. Bits are idempotent, so
+// a rank re-applying its own records changes nothing.
+__global__ void k_part_prunes_apply(uint32_t* mask, size_t mso, size_t msu, uint32_t N, uint32_t S,
+                                    const uint2* __restrict__ rec, size_t n, uint32_t* err) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const uint2 r = rec[i];
+    const uint32_t o = r.x / N, u = r.x - o * N;
+    if (o >= S) {  // a record from another engine geometry: refuse rather than write out of range
+      atomicOr(err, ERR_BOUNDS);
+      continue;
+    }
+    atomicOr(&mask[o * mso + u * msu], r.y);
+  }
+}
+
+// The prune records of this rank's round, regenerated from the received caches: a pair
+// that pruned this round (prune_round > 0) holds its prunees flagged in cache rows
+// [0, pruned-len) (ReceivedCache::prune, received_cache.rs:100-131, as k_cg_prune left
+// them); each prunee u's ring slots holding the pruner v in u's entry for the slot's
+// origin become one record (slot * N + u, bits) -- the bits PushActiveSet::prune sets
+// (push_active_set.rs:56-71). Records beyond cap are counted, not written.
+template <int ASZP>
+__global__ __launch_bounds__(256) void k_part_emit(const uint8_t* __restrict__ prune_round,
+                                                   const uint32_t* __restrict__ cmeta, const uint32_t* __restrict__ ckey,
+                                                   const uint8_t* __restrict__ bucket, const uint8_t* __restrict__ obkt,
+                                                   const uint32_t* __restrict__ peers, const uint16_t* __restrict__ hl,
+                                                   uint32_t N, uint32_t NP, uint32_t vlo, uint32_t ASZ, size_t PAIRS,
+                                                   uint2* __restrict__ rec, size_t cap, uint32_t* __restrict__ count) {
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < PAIRS; q += (size_t)gridDim.x * blockDim.x) {
+    if (!prune_round[q]) continue;
+    const uint32_t o = (uint32_t)(q / NP), v = vlo + (uint32_t)(q - (size_t)o * NP);
+    const uint32_t plen = (cmeta[q] >> 16) & 0xFFu, ob = obkt[o];
+    for (uint32_t i = 0; i < plen; ++i) {
+      const uint32_t w = ckey[(size_t)i * PAIRS + q];
+      if (!ck_pruned(w)) continue;
+      const uint32_t u = ck_id(w);
+      const uint32_t ent = u * NB + min((uint32_t)bucket[u], ob);
+      const uint32_t hv = hl[ent], head = hv & 0xFF, L = hv >> 8;
+      uint32_t row[ASZP];
+      load_row<ASZP>(peers + (size_t)ent * ASZP, row);
+      uint32_t hit = 0;
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        const uint32_t pos = (uint32_t)s >= head ? (uint32_t)s - head : (uint32_t)s + ASZ - head;
+        hit |= (uint32_t)((uint32_t)s < ASZ && pos < L && row[s] == v) << s;
+      }
+      if (!hit) continue;
+      const uint32_t k = atomicAdd(count, 1u);
+      if (k < cap) rec[k] = make_uint2(o * N + u, hit);
+    }
+  }
 }
 
 uint32_t grid_of(size_t n, uint32_t cap = 4096) {
@@ -165,31 +122,6 @@ uint32_t grid_of(size_t n, uint32_t cap = 4096) {
 }  // namespace
 
 size_t part_stats_words(const Engine& e) { return (size_t)e.S * (5 + 256 + e.bm_words); }
-
-hipError_t launch_part_begin(Engine& e) {
-  hipError_t r;
-  if ((r = hipMemsetAsync(e.hops, 0xFF, e.PAIRS, e.st)) != hipSuccess) return r;
-  if ((r = hipMemsetAsync(e.cnt, 0, e.PAIRS * 4, e.st)) != hipSuccess) return r;
-  if ((r = hipMemsetAsync(e.egress, 0, e.PAIRS, e.st)) != hipSuccess) return r;
-  if ((r = hipMemsetAsync(e.part_fr_all, 0, (size_t)e.part_K * e.S * e.part_Wr * 4, e.st)) != hipSuccess) return r;
-  hipLaunchKernelGGL(k_part_seed, dim3(grid_of(e.S)), dim3(256), 0, e.st, e.part_fr_all, e.origin, e.S, e.part_Wr,
-                     e.part_C, e.N, e.part_lo, e.part_hi, e.hops);
-  return hipGetLastError();
-}
-
-hipError_t launch_part_level(Engine& e, uint32_t d) {
-  hipError_t r;
-  if ((r = hipMemsetAsync(e.part_cnt, 0, 8, e.st)) != hipSuccess) return r;
-  hipLaunchKernelGGL(k_part_compact, dim3(grid_of((size_t)e.part_K * e.S * e.part_Wr)), dim3(256), 0, e.st,
-                     e.part_fr_all, e.part_K, e.S, e.part_Wr, e.part_C, e.N, e.q[0], e.part_cnt);
-  if ((r = hipMemsetAsync(e.part_fr_own, 0, (size_t)e.S * e.part_Wr * 4, e.st)) != hipSuccess) return r;
-  GS_ASZP_DISPATCH(e.ASZP,
-                   hipLaunchKernelGGL(k_part_expand<A>, dim3(grid_of(e.PAIRS, 2048)), dim3(256), 0, e.st, e.q[0],
-                                      e.part_cnt, d, e.bucket, e.peers, e.hl, e.frank, e.origin, e.obkt, e.nfail,
-                                      e.mask, e.hops, e.cnt, e.inb, e.egress, e.part_fr_own, e.part_cnt + 1, e.err,
-                                      e.N, e.ASZ, e.fanout, e.capin, e.PAIRS, e.part_lo, e.part_hi, e.part_Wr));
-  return hipGetLastError();
-}
 
 hipError_t launch_part_stats_pack(Engine& e) {
   hipLaunchKernelGGL(k_part_stats_pack, dim3(grid_of(part_stats_words(e))), dim3(256), 0, e.st, e.S, e.bm_words,
@@ -203,8 +135,17 @@ hipError_t launch_part_stats_unpack(Engine& e) {
   return hipGetLastError();
 }
 
-hipError_t launch_part_delta_apply(Engine& e) {
-  hipLaunchKernelGGL(k_part_delta_apply, dim3(grid_of(e.PAIRS)), dim3(256), 0, e.st, e.mask, e.part_delta, e.PAIRS);
+hipError_t launch_part_emit(Engine& e) {
+  GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_part_emit<A>, dim3(grid_of(e.PAIRS, 8192)), dim3(256), 0, e.st,
+                                              e.prune_round, e.cmeta, e.ckey, e.bucket, e.obkt, e.peers, e.hl, e.N,
+                                              e.NP, e.vlo, e.ASZ, e.PAIRS, e.part_rec, e.part_rec_cap, e.part_cnt));
+  return hipGetLastError();
+}
+
+hipError_t launch_part_prunes_apply(Engine& e, const uint2* rec, size_t n) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_part_prunes_apply, dim3(grid_of(n)), dim3(256), 0, e.st, e.mask, e.mso, e.msu, e.N, e.S, rec,
+                     n, e.err);
   return hipGetLastError();
 }
 

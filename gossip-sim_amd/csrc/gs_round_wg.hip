@@ -40,6 +40,12 @@ namespace gs {
 #endif
 constexpr uint32_t RWG_THREADS = RWG_THREADS_N;
 constexpr uint32_t RWG_WAVES = RWG_THREADS / 64;
+// Largest N whose consume CSR is staged in registers (BASELINE C2's 3,000 nodes fit);
+// larger N take the LDS-staged path. tests/test_gpu_parity.py (fused_vs_split at
+// n = 3500) covers both sides of it. Only the default 768-thread build is parity-checked.
+constexpr uint32_t RWG_CSR_REG_NODES = 3072;
+constexpr uint32_t CSR_NPT = (RWG_CSR_REG_NODES + RWG_THREADS - 1) / RWG_THREADS;  // nodes per thread
+static_assert(CSR_NPT * RWG_THREADS >= RWG_CSR_REG_NODES, "register-staged CSR covers its node bound");
 constexpr uint32_t RWG_SCR = 128;  // per-wave LDS scratch (u32): staged cache keys / prune keys
 constexpr uint32_t LANE_C = 16;    // register path: in-degree <= 16
 constexpr int LANE_L = 16;         // register prune path: cache entry <= 16 keys (the wave path
@@ -781,8 +787,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   // end of the kernel (F), since VMEM operations complete in order and a load issued
   // behind them waits for them. Two nodes per thread per step, both rows in flight.
   uint8_t* eg_l = smem + L.eg;
-  constexpr uint32_t CSR_NPT = (3072 + RWG_THREADS - 1) / RWG_THREADS;  // nodes per thread of the register-staged CSR
-  if (FP <= 8 && N <= CSR_NPT * RWG_THREADS) {
+  if (FP <= 8 && N <= RWG_CSR_REG_NODES) {
     // The push lists (in the record area) are read into registers, two u16 ids per
     // word, then after a barrier the records overwrite them: no row is read again.
     constexpr int FW = (FP + 1) / 2;

@@ -173,37 +173,40 @@ int gs_read_mst(gs_engine* e, uint32_t slot, uint32_t* parent /*[n]*/);
 int gs_kernel_time(gs_engine* e, const char* family, double* ms, uint64_t* launches);
 int gs_kernel_time_reset(gs_engine* e);
 int gs_engine_info(gs_engine* e, uint32_t* n_nodes, uint32_t* n_slots, uint32_t* bfs_mode, uint64_t* device_bytes);
+/* device_bytes split: per-(slot, node) state (hops, in-degrees, caches, counters,
+ * accumulators, record pools; a partition rank's own nodes) and everything else (rows,
+ * masks, per-node and per-slot tables, BFS queues). */
+int gs_engine_memory(gs_engine* e, uint64_t* pair_bytes, uint64_t* other_bytes);
 /* 1 if gs_round runs the one-kernel workgroup round (BFS, consume, prune and
  * statistics per slot in one workgroup), 0 if it launches the step kernels. */
 int gs_engine_round_kind(gs_engine* e, uint32_t* fused);
 
 /* --- node-range partition ------------------------------
- * K engines, one per rank/GPU, each created with bfs_mode GS_BFS_LEVEL on the same
- * stakes, slots and seed, split the node ids into K equal ranges; rank r owns
- * [r*C, min((r+1)*C, n)), C = ceil(n / K). Active sets, prune masks and failures are
- * replicated; per-(slot, node) round state, caches and accumulators are kept for owned
- * nodes only. One iteration of gossip_main.rs:449-564 is:
- *   gs_part_begin;
- *   for level d = 0, 1, ...: gs_part_level(d, &new) -> SUM(new) over ranks; stop at 0;
- *       else gs_part_frontier_out -> all-gather (rank-major) -> gs_part_frontier_in;
- *   gs_part_consume(&prunes) -> SUM(prunes); if > 0: gs_part_delta_out -> SUM ->
- *       gs_part_delta_in;
+ * K engines, one per rank/GPU, created with gs_create_part on the same stakes, params
+ * (bfs_mode GS_BFS_MULTI or AUTO), slots and seed. Rank r owns the node ids
+ * [node_lo, node_hi) (gs_part_sizes): K contiguous ranges of whole 1,024-id bins.
+ * Replicated on every rank: active sets, prune masks, failed flags (the same rotations,
+ * failures and prune bits are applied everywhere). Kept for owned nodes only: every
+ * per-(slot, node) array -- hops, in-degrees, received caches, round counters,
+ * accumulators -- i.e. S x (node_hi - node_lo) pairs. Each rank runs the whole BFS over
+ * its replicated tables (no exchange per level) and gathers, consumes and prunes for
+ * its own nodes. One iteration of gossip_main.rs:449-564 is:
+ *   gs_part_round(round, record, &n)        run_gossip + consume + send_prunes; n prune records
+ *   ALL-GATHER the ranks' records (gs_part_prunes_out, n x 2 u32 words: slot * n_nodes +
+ *       prunee, ring-slot bits) -> gs_part_prunes_in(all records)   prune_connections
  *   gs_chance_to_rotate(round);
- *   if recorded: gs_part_stats_out -> SUM -> gs_part_stats_in.
- * The exchanges are the caller's: RCCL all-gather / all-reduce on device buffers over
- * xGMI, or host buffers (dst_device / src_device select which). Buffers hold u32 words
- * (frontier, delta) and u64 words (stats); sizes from gs_part_sizes. SUM of the
- * deltas and of the stranded bitmaps equals their OR: every bit has one owner. */
-int gs_part_attach(gs_engine* e, uint32_t rank, uint32_t nranks);
-int gs_part_sizes(gs_engine* e, size_t* frontier_words /* per rank */, size_t* delta_words,
-                  size_t* stats_words, uint32_t* node_lo, uint32_t* node_hi);
-int gs_part_begin(gs_engine* e);
-int gs_part_level(gs_engine* e, uint32_t level, uint32_t* new_local);
-int gs_part_frontier_out(gs_engine* e, void* dst, int dst_device);       /* [S][Wr] u32 */
-int gs_part_frontier_in(gs_engine* e, const void* src, int src_device);  /* [K][S][Wr] u32 */
-int gs_part_consume(gs_engine* e, uint32_t* local_prunes);
-int gs_part_delta_out(gs_engine* e, void* dst, int dst_device);          /* [S][n] u32 */
-int gs_part_delta_in(gs_engine* e, const void* src, int src_device);
+ *   if recorded: gs_part_stats_out -> SUM over ranks -> gs_part_stats_in.
+ * The exchanges are the caller's: RCCL on device buffers over xGMI, or host buffers
+ * (dst_device / src_device select which). Readbacks of per-pair arrays fill the owned
+ * nodes (hops 0xFF, counters 0 and empty caches elsewhere); gs_round and the step-wise
+ * calls (gs_run_gossip ...) return GS_ESTATE on a partition rank.
+ * Replaces: the same loop as gs_round over one engine (results identical on owned nodes). */
+int gs_create_part(const gs_params* params, const uint64_t* stakes, uint32_t n_nodes, uint32_t n_slots,
+                   uint32_t rank, uint32_t nranks, gs_engine** out);
+int gs_part_sizes(gs_engine* e, size_t* stats_words, uint32_t* node_lo, uint32_t* node_hi);
+int gs_part_round(gs_engine* e, uint32_t round, int record, uint32_t* n_records);
+int gs_part_prunes_out(gs_engine* e, void* dst, int dst_device);                 /* [n_records][2] u32 */
+int gs_part_prunes_in(gs_engine* e, const void* src, size_t n_records, int src_device);
 int gs_part_stats_out(gs_engine* e, void* dst, int dst_device);          /* [S][5 + 256 + W] u64 */
 int gs_part_stats_in(gs_engine* e, const void* src, int src_device);
 

@@ -1,13 +1,16 @@
-"""Node-range partition: two ranks, each owning half of the node
-ids, exchange frontier bitsets per BFS level, prune-mask deltas and statistics partials
-through torch.distributed (gloo, host buffers) and must reproduce one engine over all
+"""Node-range partition: two ranks, each owning a contiguous half
+of the node ids (whole 1,024-id bins), keep per-(slot, node) state for their own nodes
+only, run the whole multi-source BFS over replicated rows, exchange prune records and
+statistics partials through torch.distributed, and must reproduce one engine over all
 nodes bit for bit: per-round summaries, hop-histogram accumulators, replicated prune
-masks, and -- on each rank's own nodes -- hops, message accumulators and caches.
+masks, and -- on each rank's own nodes -- hops, message accumulators and caches. Each
+rank's device memory is its half of the per-pair state plus the replicated tables.
 
-Both ranks run on the one GPU of the box (two engines on device 0); the RCCL path is
-the same call sequence with device buffers.
-"""
+Both ranks run on the one GPU of the box (two engines on device 0): gloo exchanges host
+buffers; nccl (RCCL) exchanges device buffers when RCCL accepts two ranks on one GPU
+(otherwise the case is skipped with that reason)."""
 import os
+import pickle
 import socket
 import subprocess
 import sys
@@ -16,9 +19,10 @@ import numpy as np
 import pytest
 
 import engine_bind as eb
-from partition_case import CASE, run_case
+from partition_case import CASES, cache_rows, run_case, stakes_of
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+RCCL_REFUSED = 77
 
 
 def free_port():
@@ -27,33 +31,69 @@ def free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.gpu
-def test_partition_two_ranks_matches_one_engine(tmp_path):
-    world, port = 2, free_port()
+def run_ranks(tmp_path, case, backend, world=2):
+    port = free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), GS_PART_OUT=str(tmp_path / f"rank{r}.npz"))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "partition_worker.py")], env=env,
+                   MASTER_PORT=str(port), GS_PART_OUT=str(tmp_path / f"rank{r}.npz"), GS_PART_CASE=case,
+                   GS_PART_BACKEND=backend)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "partition_worker.py")], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
-    logs = [p.communicate(timeout=240)[0] for p in procs]
+    try:
+        logs = [p.communicate(timeout=400)[0] for p in procs]
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            p.kill()
+        for p in procs:
+            p.communicate()
+        raise
+    if backend == "nccl" and any(p.returncode == RCCL_REFUSED for p in procs):
+        pytest.skip("RCCL refused two ranks on the box's one GPU: " + " | ".join(l.strip()[-300:] for l in logs))
     for p, log in zip(procs, logs):
         assert p.returncode == 0, log[-3000:]
-
-    st = eb.synth.network(CASE["n"])[1]
-    one = eb.gs.Engine(st, len(CASE["origins"]), bfs_mode=eb.gs.GS_BFS_LEVEL, seed=CASE["seed"],
-                       rotation_probability=CASE["p"])
-    want = run_case(one)
     parts = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
-    assert sum(int(p["hi"][0]) - int(p["lo"][0]) for p in parts) == CASE["n"]
+    caches = []
+    for r in range(world):
+        with open(tmp_path / f"rank{r}.npz.caches", "rb") as f:
+            caches.append(pickle.load(f))
+    return parts, caches
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,backend", [("small", "gloo"), ("small", "nccl"), ("large", "gloo")])
+def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend):
+    parts, caches = run_ranks(tmp_path, case, backend)
+    c = CASES[case]
+    st = stakes_of(case, eb.synth)
+    S = len(c["mi"])
+    one = eb.gs.Engine(st, S, bfs_mode=eb.gs.GS_BFS_LEVEL, seed=c["seed"], rotation_probability=c["p"])
+    want = run_case(one, case, st)
+    want_caches = {k: cache_rows(one, case, k) for k in range(S)}
+    one.close()
+    assert sum(int(p["hi"][0]) - int(p["lo"][0]) for p in parts) == c["n"]
     assert want["summaries"]["prunes"].sum() > 0 and want["summaries"]["stranded"].sum() > 0
     for p in parts:
         np.testing.assert_array_equal(p["summaries"], want["summaries"])
-    for k in range(len(CASE["origins"])):
+    for k in range(S):
         np.testing.assert_array_equal(sum(p[f"acc{k}"] for p in parts), want[f"acc{k}"], err_msg=f"slot {k}")
-        for p in parts:
+        for r, p in enumerate(parts):
             lo, hi = int(p["lo"][0]), int(p["hi"][0])
             np.testing.assert_array_equal(p[f"hist{k}"], want[f"hist{k}"])
             np.testing.assert_array_equal(p[f"pruned{k}"], want[f"pruned{k}"], err_msg=f"masks slot {k}")
             np.testing.assert_array_equal(p[f"hops{k}"][lo:hi], want[f"hops{k}"][lo:hi])
-            np.testing.assert_array_equal(p[f"cache{k}"][lo:hi], want[f"cache{k}"][lo:hi], err_msg=f"cache {k}")
+            if f"cache{k}" in want:
+                np.testing.assert_array_equal(p[f"cache{k}"][lo:hi], want[f"cache{k}"][lo:hi], err_msg=f"cache {k}")
+            for v, row in caches[r][k].items():
+                assert row == want_caches[k][v], f"cache slot {k} node {v}"
+    if case == "large":
+        # device memory per rank: its share of the per-(slot, node) state + the replicated tables
+        full = eb.gs.Engine(st, S, bfs_mode=eb.gs.GS_BFS_MULTI, seed=c["seed"], rotation_probability=c["p"])
+        fi = full.info()
+        full.close()
+        for p in parts:
+            dev, pair, other = (int(x) for x in p["bytes"])
+            share = (int(p["hi"][0]) - int(p["lo"][0])) / c["n"]
+            assert abs(pair - share * fi["pair_bytes"]) <= 0.01 * fi["pair_bytes"] + (64 << 20), (pair, fi)
+            assert abs(other - fi["other_bytes"]) <= 0.02 * fi["other_bytes"], (other, fi)
+            assert dev < 0.8 * fi["device_bytes"], (dev, fi)
