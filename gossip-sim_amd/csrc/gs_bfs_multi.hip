@@ -674,10 +674,13 @@ __device__ inline void mv_pair_records(const MvCsr& L, uint32_t r0, uint32_t r1,
   const uint32_t Ln = r1 - r0;
   uint32_t blo = 0, bhi = 0;
   c = 0;
-  if (Ln <= 64) {
-    const uint32_t l1 = min(Ln, 32u);
-    for (uint32_t k = 0; k < l1; ++k) blo |= ((L.msk[r0 + k] >> j) & 1u) << k;
-    for (uint32_t k = 32; k < Ln; ++k) bhi |= ((L.msk[r0 + k] >> j) & 1u) << (k - 32);
+  if (Ln <= 64) {  // 4 independent LDS loads per step (the list is followed by >= 3 readable words)
+    for (uint32_t k = 0; k < Ln; k += 4) {
+      const uint32_t m0 = L.msk[r0 + k], m1 = L.msk[r0 + k + 1], m2 = L.msk[r0 + k + 2], m3 = L.msk[r0 + k + 3];
+      const uint32_t b = ((m0 >> j) & 1u) | (((m1 >> j) & 1u) << 1) | (((m2 >> j) & 1u) << 2) | (((m3 >> j) & 1u) << 3);
+      const uint32_t bm = Ln - k >= 4 ? b : b & ((1u << (Ln - k)) - 1);
+      if (k < 32) blo |= bm << k; else bhi |= bm << (k - 32);
+    }
     c = (uint32_t)(__popc(blo) + __popc(bhi));
   } else {
     for (uint32_t r = r0; r < r1; ++r) {
@@ -714,9 +717,10 @@ __device__ inline uint32_t mv_pair_hop(const MvCsr& L, uint32_t r0, uint32_t r1,
   return mh;
 }
 
-// Per (slot, node) of the fine bin: in-degree, the inbound rows and the hop, coalesced
-// over nodes (the step API's gs_run_gossip; gs_round fuses this with consume below).
-// Row t of every lane's pair is stored by one wave instruction (t = 0, 1, ...).
+// Per (slot, node) of the fine bin: in-degree, the inbound rows and the hop (the step
+// API's gs_run_gossip, and gs_round unless GS_MV_FUSED=1). A lane appends its pair's
+// records as it finds them (rows of different lanes differ: measured faster than
+// filtering to a bitmap and storing row t of every lane together, 568 vs 697 us at C4).
 __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t f = mv_xcd_bin(blockIdx.x, a.fno);  // local kept-bin index
@@ -727,35 +731,21 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
   const MvCsr L = mv_csr_lds(smem, BP, gcap);
   bool over = false;
   mv_bin_csr(a, f, nlev, nv, gcap, L, [&](uint32_t lo, uint32_t hi, uint32_t base) {
-    for (uint32_t i0 = lo; i0 < hi; i0 += MV_GT) {  // block-uniform trip count (whole waves below)
-      const uint32_t i = i0 + tid;
-      const bool in = i < hi;
-      const uint32_t v = v0 + i;
-      const uint32_t r0 = in ? L.cn[i] - base : 0u, r1 = in ? min(L.cn[i + 1] - base, gcap) : 0u;
+    for (uint32_t i = lo + tid; i < hi; i += MV_GT) {
+      const uint32_t v = v0 + i, r0 = L.cn[i] - base, r1 = min(L.cn[i + 1] - base, gcap);
       for (uint32_t j = 0; j < Sg; ++j) {
         const size_t p = (size_t)(a.s0 + j) * a.NP + (v - a.vlo);
-        uint32_t rk[16], cc;
-        mv_pair_records(L, r0, r1, j, rk, cc);
-        const uint32_t wc = min(active_max<7>(min(cc, 127u)), min(16u, a.capin));
-#pragma unroll
-        for (uint32_t t = 0; t < 16; ++t) {
-          if (t >= wc) break;
-          if (t < cc) a.inb[(size_t)t * a.PAIRS + p] = rk[t];
+        uint32_t cc = 0, mh = 0xFFu;
+        for (uint32_t r = r0; r < r1; ++r) {
+          if (!((L.msk[r] >> j) & 1u)) continue;
+          const uint32_t key = L.keys[r];
+          if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = key;
+          mh = min(mh, key >> 24);
+          ++cc;
         }
-        if (cc > 16) {  // (rare) rows 16 .. : the matches after the 16th, in list order
-          uint32_t k = 0;
-          for (uint32_t r = r0; r < r1; ++r) {
-            if (!((L.msk[r] >> j) & 1u)) continue;
-            if (k >= 16 && k < a.capin) a.inb[(size_t)k * a.PAIRS + p] = L.keys[r];
-            ++k;
-          }
-        }
-        const uint32_t mh = mv_pair_hop(L, r0, r1, j, rk, cc);
-        if (in) {
-          over |= cc > a.capin;
-          a.cnt[p] = cc;
-          a.hops[p] = (uint8_t)(v == L.sorg[j] ? 0u : (cc ? mh : 0xFFu));
-        }
+        over |= cc > a.capin;
+        a.cnt[p] = cc;
+        a.hops[p] = (uint8_t)(v == L.sorg[j] ? 0u : (cc ? mh : 0xFFu));
       }
     }
   });
@@ -920,8 +910,9 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   g.rows_cap = (g.q_cap + MV_XT - 1) / MV_XT + 1;
   const size_t rpn = (size_t)ASZ * std::min<size_t>(sg, 4) + 16;  // pool records per node (average over a bin)
   g.pcap = ((size_t)1 << g.BSF) * rpn;
-  g.gcap = (uint32_t)((MV_GLDS - mv_gather_fixed_bytes(g.BSF)) / 8);
-  g.gcap_c = (uint32_t)((MV_GLDS - MV_CSCR - mv_gather_fixed_bytes(g.BSF)) / 8);
+  // (2 records' worth of slack: the filter reads up to 3 words past a node's list)
+  g.gcap = (uint32_t)((MV_GLDS - mv_gather_fixed_bytes(g.BSF)) / 8) - 2;
+  g.gcap_c = (uint32_t)((MV_GLDS - MV_CSCR - mv_gather_fixed_bytes(g.BSF)) / 8) - 2;
 }
 
 bool mv_supported(const MvGeom& g, uint32_t ASZP) {

@@ -298,7 +298,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   if (mode == GS_BFS_MULTI) {
     const MvGeom& g = e->mv;
     if (const char* dg = std::getenv("GS_MV_DIAG"); dg && dg[0] == '1') e->mv_diag = true;
-    if (const char* fu = std::getenv("GS_MV_FUSED"); fu && fu[0] == '0') e->mv_fused = false;
+    if (const char* fu = std::getenv("GS_MV_FUSED"); fu && fu[0] == '1') e->mv_fused = true;
     e->ORW = ((e->ASZP + 1 + e->ASZP / 4) + 3) & ~3u;  // row, meta, the peers' failure classes
     ALLOC(e->own, N * e->ORW, 0);
     ALLOC(e->mv_vis, N, 0);

@@ -10,7 +10,7 @@ if [ -n "$PARITY_K" ]; then
   rc=$?; tail -3 $OUT/parity_ab.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 fi
-for fu in 1 0; do
+for fu in 0 1; do
   GS_MV_FUSED=$fu timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_ab$fu -o run -- \
     python3 bench.py --only-large --large-mode 4 > $OUT/ab$fu.json 2>&1 || exit $?
   echo "== fused=$fu"; grep -o '"c4".*"bfs_roofline"' $OUT/ab$fu.json
