@@ -152,3 +152,61 @@ def test_sharded_sweep_gpu_world2_matches_one_process():
     outs = _run_world(2, use_gpu=True)
     for got in outs:
         _check(got, want)
+
+
+# ---- origin sharding of ONE network (bench.py --shard-origins, strong scaling) ----
+SH_N, SH_ORIGINS, SH_ROUNDS = 120, 7, 24
+
+
+def _origin_rows(origins):
+    """Per round, per origin: (pushes, nodes reached) of the oracle's Cluster run over the
+    shared seed -- 8 bytes per origin, the unit that bench.py's shard check reassembles."""
+    import oracle_bind as ob
+    pks, st = eb.synth.network(SH_N)
+    rows = np.zeros((SH_ROUNDS, len(origins), 2), dtype=np.uint32)
+    for j, o in enumerate(origins):
+        sim = ob.Sim(ob.PHILOX, 7, pks, st, 6)
+        sim.init_philox(12)
+        for r in range(SH_ROUNDS):
+            rows[r, j, 0] = sim.round(o, 0.15, 2, 12, 0.05, r)
+            rows[r, j, 1] = int((sim.distances() != np.iinfo(np.uint64).max).sum())
+    return rows.view(np.uint8).reshape(SH_ROUNDS, -1)
+
+
+def _shard_worker(rank, world, port, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.dirname(here)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as tdist
+    import engine_bind  # noqa: F401
+    import gossip_sim_amd.sweep as sw
+    from test_sweep_dist import SH_ORIGINS, _origin_rows
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    lo, hi = sw.shard_range(SH_ORIGINS, rank, world)
+    local = _origin_rows(list(range(lo, hi)))
+    full = sw.gather_rows((torch, tdist), local, SH_ORIGINS, world, row_bytes=8)
+    np.save(os.path.join(outdir, f"rank{rank}.npy"), full)
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_origin_shard_reassembly_gloo_world2():
+    """--shard-origins: each rank runs a contiguous share of the origins of one network
+    (shard_range; the same seed, so the same active-set trajectory), and gather_rows
+    reassembles every origin's per-round rows on every rank, bit-identical to one
+    process running all origins."""
+    import torch.multiprocessing as mp
+    for n in (0, 1, 7, 3000):
+        for world in (1, 2, 3, 8):
+            spans = [sweep.shard_range(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    want = _origin_rows(list(range(SH_ORIGINS)))
+    d = tempfile.mkdtemp()
+    mp.spawn(_shard_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+    for r in range(2):
+        got = np.load(os.path.join(d, f"rank{r}.npy"))
+        assert got.tobytes() == want.tobytes()
