@@ -193,12 +193,20 @@ __device__ inline uint32_t off_fetch_inc(uint32_t* offw, uint32_t w, bool pu, ui
 
 // Bit j set when record j's id (low 16 bits of rk[j]) equals k, for j < NC (records
 // past the in-degree are 0xFFFFFFFF and their bits are never consulted).
-template <int NC>
-__device__ inline uint32_t match_ids(const uint32_t (&rk)[16], uint32_t k) {
-  uint32_t m = 0;
+typedef unsigned short rwg_u16x2 __attribute__((ext_vector_type(2)));
+
+// Presence of record ids (u16: N < 2^16 here) in the cache entry, two records per
+// register: x = pair ^ (key | key << 16) has a zero half where the key matches, and a
+// packed u16 min (one v_pk_min_u16) keeps, per half, the smallest x seen -- zero iff
+// that record's id is in the entry. One xor and one min per key per TWO records.
+template <int NP2>
+__device__ inline void match_pairs(const uint32_t (&pk)[8], uint32_t k2, uint32_t (&mn)[8]) {
 #pragma unroll
-  for (int j = 0; j < NC; ++j) m |= (uint32_t)((rk[j] & 0xFFFFu) == k) << j;
-  return m;
+  for (int h = 0; h < NP2; ++h) {
+    const uint32_t x = pk[h] ^ k2;
+    const rwg_u16x2 m = __builtin_elementwise_min(__builtin_bit_cast(rwg_u16x2, mn[h]), __builtin_bit_cast(rwg_u16x2, x));
+    mn[h] = __builtin_bit_cast(uint32_t, m);
+  }
 }
 
 // ---- C: register path (1 <= c <= 16) ----
@@ -221,8 +229,17 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
   if (wc <= 4) sort_net<4>(rk);
   else if (wc <= 8) sort_net<8>(rk);
   else sort_net<16>(rk);
+  // ids of ranks 2h, 2h + 1 in one register (padding ranks carry 0xFFFF, which no key
+  // below equals: ids are < N <= 65,535 and an unused row reads as 0xFFFF)
+  uint32_t pk[8], mn[8];
+#pragma unroll
+  for (int h = 0; h < 8; ++h) {
+    pk[h] = (rk[2 * h] & 0xFFFFu) | (rk[2 * h + 1] << 16);
+    mn[h] = 0xFFFFFFFFu;
+  }
+  const uint32_t id0 = rk[0] & 0xFFFFu, id1 = rk[1] & 0xFFFFu;
   // look the records up in the entry: rows streamed 8 at a time, loads issued together
-  uint32_t present = 0, w0 = 0, w1 = 0;
+  uint32_t w0 = 0, w1 = 0;
   int idx0 = -1, idx1 = -1;
   const uint32_t wl = active_max<7>(len);
   for (uint32_t i0 = 0; i0 < wl; i0 += 8) {
@@ -233,13 +250,20 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const uint32_t i = i0 + t;
-      const uint32_t k = i < len ? ck_id(kc[t]) : 0xFFFFFFFEu;  // never equals a u16 record id
-      const uint32_t m = wc <= 4 ? match_ids<4>(rk, k) : wc <= 8 ? match_ids<8>(rk, k) : match_ids<16>(rk, k);
-      present |= m;
-      if (m & 1u) { idx0 = (int)i; w0 = kc[t]; }
-      if (m & 2u) { idx1 = (int)i; w1 = kc[t]; }
+      const uint32_t k = i < len ? ck_id(kc[t]) : 0xFFFFu;
+      const uint32_t k2 = k | (k << 16);
+      if (wc <= 4) match_pairs<2>(pk, k2, mn);
+      else if (wc <= 8) match_pairs<4>(pk, k2, mn);
+      else match_pairs<8>(pk, k2, mn);
+      if (k == id0) { idx0 = (int)i; w0 = kc[t]; }
+      if (k == id1) { idx1 = (int)i; w1 = kc[t]; }
     }
   }
+  uint32_t present = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) present |= (uint32_t)(((mn[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) == 0u) << j;
+  idx0 = c > 0 ? idx0 : -1;
+  idx1 = c > 1 ? idx1 : -1;
   up = up < 255 ? up + 1 : 255;  // rank 0 (received_cache.rs:84-86)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {  // timely: score += 1, inserted regardless of the 50-key cap
