@@ -347,7 +347,7 @@ def main():
         roof = roofline(bp, k_ms, k_n, "BFS", "B_prop (SURVEY 8d)")
     phases = None
     if os.environ.get("GS_PHASE_PROFILE") == "1" and fused:  # workgroup-ms per k_round_wg phase
-        names = ["init", "bfs", "csr_stats", "consume_prune", "heavy", "summary"]
+        names = ["init", "bfs", "csr_stats", "consume_prune", "heavy", "outputs_stats", "summary"]
         phases = {nm: round(eng.kernel_time("phase." + chr(65 + i))[0], 2) for i, nm in enumerate(names)}
     shard_check = None
     if args.shard_origins and world > 1:

@@ -938,6 +938,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   }
   if (npr_sum) atomicAdd(&ctrl[C_PRUNES], npr_sum);
   if (errf) atomicOr(&ctrl[C_ERR], errf);
+  RWG_MARK(4);
 
   // ---------------- F: per-pair outputs and measured-round statistics --------
   // (gossip_main.rs:480-514) Stranded nodes' stake/rank loads go first, then only
@@ -981,7 +982,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
     }
   }
   __syncthreads();
-  RWG_MARK(4);
+  RWG_MARK(5);
 
   // ---------------- E: slot summary -----------------------------------------
   if (tid == 0) {
@@ -1023,7 +1024,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
     }
     a.sum[o] = s;
   }
-  RWG_MARK(5);
+  RWG_MARK(6);
 }
 
 template <int ASZP, bool OFF16, int FP>
