@@ -185,11 +185,12 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
             "edges_per_s": E / dt, "origin_rounds_per_s": S * steps / dt,
             "pushes_per_origin_round": E / (S * steps),
             "us_per_round": {k: round(v * 1e3 / steps, 1) for k, v in fam.items()},
-            # multi: the gather that writes hops / in-degrees runs fused with consume; its whole
-            # time is charged to the BFS (conservative: the consume work inside it is counted too)
+            # multi: the level loop plus the gather that writes hops / in-degrees / inbound rows
+            # (with GS_MV_FUSED=1 the gather runs fused with consume, and its whole time is charged)
             "bfs_roofline": roofline(bp, fam["bfs"] + fam.get("gather", 0.0) + fam.get("gather_consume", 0.0), steps,
-                                     f"BFS ({mode}: " + ("expand/apply per level + fused gather/consume)" if mode == "multi"
-                                                         else "per level)"),
+                                     f"BFS ({mode}: " + ("expand/apply per level + " +
+                                                         ("fused gather/consume)" if "gather_consume" in fam
+                                                          else "gather)") if mode == "multi" else "per level)"),
                                      "B_prop (SURVEY 8d), summed over slots", f"bfs_{mode}_c4")}
 
 
