@@ -85,6 +85,8 @@ struct MvArgs {
   // A node-range partition rank runs the whole BFS but keeps the records, counts and
   // egress of its own nodes only.
   uint32_t vlo, vhi, flo, fno, NP;
+  uint32_t MSU;  // node stride of the masks (SP, or 32 in node lines)
+  uint32_t small;  // levels of at most this many entries run in the one-workgroup kernel
   size_t PAIRS, area_cap, rows_cap, q_cap, pcap;
 };
 
@@ -154,7 +156,7 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const uint32_
     }
   }
   uint4 m4[MV_SG4];
-  const uint4* mq = reinterpret_cast<const uint4*>(a.mask + (size_t)u * a.SP + a.s0);
+  const uint4* mq = reinterpret_cast<const uint4*>(a.mask + (size_t)u * a.MSU + a.s0);  // (same line as the row)
 #pragma unroll
   for (uint32_t q = 0; q < MV_SG4; ++q) m4[q] = (q < nq && ((M >> (4 * q)) & 0xFu)) ? mq[q] : make_uint4(0, 0, 0, 0);
   uint32_t hv = tail[0] & 0xFFFFu;
@@ -436,7 +438,7 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint2*
 
 // ------------------------------------------------------------ small levels ----
 constexpr uint32_t MV_ST = 1024;     // threads of the small-level workgroup
-constexpr uint32_t MV_SMALL = 4096;  // frontier entries at most for a small level
+constexpr uint32_t MV_SMALL = 1024;  // frontier entries at most for a small level (default; GS_MV_SMALL): C4 917 us vs 936 at 4096
 
 template <class T>
 __device__ inline T mv_ld(T* p) {  // device-scope load: lines updated by atomics elsewhere
@@ -462,7 +464,7 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2
   }
   for (uint32_t i = tid; i < GT_WORDS; i += MV_ST) gt[i] = a.gt[i];
   uint32_t d = d0, qn = a.lvl[d0];
-  while (qn > 0 && qn <= MV_SMALL && d < 254) {
+  while (qn > 0 && qn <= a.small && d < 254) {
     uint2* qcur = (d & 1) ? q1 : q0;
     uint2* qnxt = (d & 1) ? q0 : q1;
     for (uint32_t f = tid; f < a.fno; f += MV_ST) snap[f] = mv_ld(&a.pused[f]);
@@ -990,7 +992,9 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.pool = e.mv_pool; a.pused = e.mv_pused; a.Lt = e.mv_Lt;
   a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
-  a.vlo = e.vlo; a.vhi = e.vlo + e.NP; a.NP = e.NP;
+  a.vlo = e.vlo; a.vhi = e.vlo + e.NP; a.NP = e.NP; a.MSU = (uint32_t)e.msu;
+  a.small = MV_SMALL;
+  if (const char* sm = std::getenv("GS_MV_SMALL")) a.small = (uint32_t)std::strtoul(sm, nullptr, 10);
   a.flo = e.vlo >> e.mv.BSF; a.fno = mv_kept_bins(e);
   a.ORW = e.ORW;
   a.any_fail = 0;
@@ -1089,7 +1093,7 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
           uint32_t x = 0;
           if ((r = mv_wait(hl + (d - 2), e.st, x))) return r;
           if (x == 0) { nlev = d + 1; done = true; break; }
-          if (x <= MV_SMALL) { ++d; break; }  // levels d - 1, d are enqueued; small levels from d + 1
+          if (x <= a.small) { ++d; break; }  // levels d - 1, d are enqueued; small levels from d + 1
         }
       }
       if (done) break;

@@ -248,6 +248,15 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   e->SP = (uint32_t)((S + 3) & ~(size_t)3);
   if (mode == GS_BFS_MULTI) {  // node-major masks / egress: a node's slots share one line
     e->mso = 1; e->msu = e->SP; e->eso = 1; e->esu = e->SP; e->mask_words = N * e->SP;
+    // node lines: when a node's own-entry row and its masks fit 128 B, both live in one
+    // line of the row table (stride 32 words, masks at the row's end): an expansion
+    // reads one HBM line per entry instead of two half-used ones
+    const uint32_t row_words = ((e->ASZP + 1 + e->ASZP / 4) + 3) & ~3u;
+    const char* nl = std::getenv("GS_MV_NO_LINE");
+    if (row_words + e->SP <= 32 && !(nl && nl[0] == '1')) {
+      e->mv_line = true;
+      e->msu = 32;
+    }
   } else {
     e->mso = N; e->msu = 1; e->eso = N; e->esu = 1; e->mask_words = PAIRS;
   }
@@ -269,7 +278,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   ALLOC(e->thr, S, 0);
   ALLOC(e->nfail, S, 0);
   ALLOC(e->slot_prunes, S, 0);
-  ALLOC(e->mask, e->mask_words, 0);
+  if (!e->mv_line) ALLOC(e->mask, e->mask_words, 0);  // (node lines: inside the row table below)
   size_t b0 = e->dev_bytes;  // per-(slot, node) state from here (a partition rank: its own nodes)
   ALLOC(e->hops, PAIRS, 0xFF);
   ALLOC(e->cnt, PAIRS, 0);
@@ -302,8 +311,10 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     const MvGeom& g = e->mv;
     if (const char* dg = std::getenv("GS_MV_DIAG"); dg && dg[0] == '1') e->mv_diag = true;
     if (const char* fu = std::getenv("GS_MV_FUSED"); fu && fu[0] == '1') e->mv_fused = true;
-    e->ORW = ((e->ASZP + 1 + e->ASZP / 4) + 3) & ~3u;  // row, meta, the peers' failure classes
+    const uint32_t row_words = ((e->ASZP + 1 + e->ASZP / 4) + 3) & ~3u;  // row, meta, peers' failure classes
+    e->ORW = e->mv_line ? 32 : row_words;
     ALLOC(e->own, N * e->ORW, 0);
+    if (e->mv_line) e->mask = e->own + row_words;
     ALLOC(e->mv_vis, N, 0);
     ALLOC(e->mv_q[0], g.q_cap, 0);
     ALLOC(e->mv_q[1], g.q_cap, 0);
@@ -409,8 +420,15 @@ void gs_destroy(gs_engine* eh) { destroy_engine(reinterpret_cast<Engine*>(eh)); 
   if (!e) return fail(GS_EINVAL, "null engine");                \
   HIPC(hipSetDevice(e->prm.device));
 
+// Zeroes every prune mask (in the multi BFS's node lines, only the mask words).
+static hipError_t clear_masks(Engine* e) {
+  if (e->mv_line)
+    return hipMemset2DAsync(e->mask, (size_t)e->msu * 4, 0, (size_t)e->SP * 4, e->N, e->st);
+  return hipMemsetAsync(e->mask, 0, e->mask_words * 4, e->st);
+}
+
 static int reset_pair_state(Engine* e) {
-  HIPC(hipMemsetAsync(e->mask, 0, e->mask_words * 4, e->st));
+  HIPC(clear_masks(e));
   HIPC(hipMemsetAsync(e->cmeta, 0, e->PAIRS * 4, e->st));
   HIPC(hipMemsetAsync(e->egress_acc, 0, e->PAIRS * 4, e->st));
   HIPC(hipMemsetAsync(e->ingress_acc, 0, e->PAIRS * 4, e->st));
@@ -472,7 +490,7 @@ int gs_init_active_sets(gs_engine* eh) {
   ENGINE(eh);
   if (int s_ = flush_rot_clear(e)) return s_;
   HIPC(launch_init_entries(*e));
-  HIPC(hipMemsetAsync(e->mask, 0, e->mask_words * 4, e->st));
+  HIPC(clear_masks(e));
   return GS_OK;
 }
 

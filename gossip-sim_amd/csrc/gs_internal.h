@@ -125,6 +125,7 @@ struct Engine {
   std::vector<MvGroup> mv_groups;
   bool mv_attr_set = false;
   bool mv_diag = false;  // GS_MV_DIAG=1
+  bool mv_line = false;   // multi: prune masks live in the row table's node lines (msu = 32)
   bool mv_fused = false;  // gs_round: gather, then k_cg_consume; GS_MV_FUSED=1: fused gather + consume (slower at C4)
   std::vector<uint32_t> h_nfail_any;  // host copy: slot has failed nodes
   // rotation
