@@ -738,12 +738,17 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
       for (uint32_t j = 0; j < Sg; ++j) {
         const size_t p = (size_t)(a.s0 + j) * a.NP + (v - a.vlo);
         uint32_t cc = 0, mh = 0xFFu;
-        for (uint32_t r = r0; r < r1; ++r) {
-          if (!((L.msk[r] >> j) & 1u)) continue;
-          const uint32_t key = L.keys[r];
-          if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = key;
-          mh = min(mh, key >> 24);
-          ++cc;
+        for (uint32_t r = r0; r < r1; r += 4) {  // 8 LDS loads, then one wait (>= 2 records of slack follow the CSR)
+          uint32_t m[4], k[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) { m[t] = L.msk[r + t]; k[t] = L.keys[r + t]; }
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (r + t >= r1 || !((m[t] >> j) & 1u)) continue;
+            if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = k[t];
+            mh = min(mh, k[t] >> 24);
+            ++cc;
+          }
         }
         over |= cc > a.capin;
         a.cnt[p] = cc;
@@ -912,9 +917,9 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   g.rows_cap = (g.q_cap + MV_XT - 1) / MV_XT + 1;
   const size_t rpn = (size_t)ASZ * std::min<size_t>(sg, 4) + 16;  // pool records per node (average over a bin)
   g.pcap = ((size_t)1 << g.BSF) * rpn;
-  // (2 records' worth of slack: the filter reads up to 3 words past a node's list)
-  g.gcap = (uint32_t)((MV_GLDS - mv_gather_fixed_bytes(g.BSF)) / 8) - 2;
-  g.gcap_c = (uint32_t)((MV_GLDS - MV_CSCR - mv_gather_fixed_bytes(g.BSF)) / 8) - 2;
+  // (4 records' worth of slack: the filters read up to 3 records past a node's list)
+  g.gcap = (uint32_t)((MV_GLDS - mv_gather_fixed_bytes(g.BSF)) / 8) - 4;
+  g.gcap_c = (uint32_t)((MV_GLDS - MV_CSCR - mv_gather_fixed_bytes(g.BSF)) / 8) - 4;
 }
 
 bool mv_supported(const MvGeom& g, uint32_t ASZP) {

@@ -277,6 +277,34 @@ def test_fused_round_matches_steps(mode, narrow):
     np.testing.assert_array_equal(a.summaries(), b.summaries())
 
 
+@pytest.mark.parametrize("narrow", [False, True])
+def test_multi_fused_gather_consume_matches_steps(narrow, monkeypatch):
+    """GS_MV_FUSED=1: the multi-source BFS's gs_round consumes straight from the gather's
+    LDS CSR (k_mv_consume: register, wave and serial paths with narrow bounds) -- equal
+    to the step-by-step calls, as the default gather + k_cg_consume round is."""
+    monkeypatch.setenv("GS_MV_FUSED", "1")
+    pks, st = eb.synth.network(260)
+    a = gs.Engine(st, 4, seed=3, rotation_probability=0.05, narrow_wave_path=narrow, bfs_mode=gs.GS_BFS_MULTI)
+    monkeypatch.delenv("GS_MV_FUSED")
+    b = gs.Engine(st, 4, seed=3, rotation_probability=0.05, bfs_mode=gs.GS_BFS_MULTI)
+    for e in (a, b):
+        e.set_slots([0, 10, 100, 200], [2, 0, 2, 1], [0.15, 0.0, 0.5, 0.05])
+        e.init_active_sets()
+    for r in range(30):
+        a.round(r, record=r >= 10)
+        b.run_gossip(); b.consume_messages(); b.send_prunes(); b.prune_connections(); b.chance_to_rotate(r)
+        if r >= 10:
+            b.record_round()
+    for k in range(4):
+        np.testing.assert_array_equal(a.hops(k), b.hops(k))
+        np.testing.assert_array_equal(a.pruned_all(k), b.pruned_all(k))
+        for x, y in zip(a.caches(k), b.caches(k)):
+            np.testing.assert_array_equal(x, y)
+        for x, y in zip(a.accumulators(k), b.accumulators(k)):
+            np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(a.summaries(), b.summaries())
+
+
 # --------------------------------------------------------- whole simulation ----
 F64_NAMES = ["coverage", "rmr", "branching", "hop_mean", "hop_median", "coverage_stats", "rmr_stats",
              "branching_stats", "aggregate_hops", "ldh", "stranded", "stranded_round_mean", "stranded_round_median"]
