@@ -175,6 +175,10 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
     for k in ("gather", "gather_consume"):
         if not fam[k]:
             del fam[k]
+    phases = None
+    if os.environ.get("GS_PHASE_PROFILE") == "1":  # multi gather: workgroup-ms per phase (thread 0 of each workgroup)
+        names = {12: "count", 13: "scan_place", 14: "body_light", 15: "body_all"}
+        phases = {nm: round(eng.kernel_time("phase." + chr(65 + i))[0], 2) for i, nm in names.items()}
     info = eng.info()
     eng.close()
     mode = {2: "level", 3: "binned", 4: "multi"}.get(info["bfs_mode"], str(info["bfs_mode"]))
@@ -185,6 +189,7 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
             "edges_per_s": E / dt, "origin_rounds_per_s": S * steps / dt,
             "pushes_per_origin_round": E / (S * steps),
             "us_per_round": {k: round(v * 1e3 / steps, 1) for k, v in fam.items()},
+            **({"gather_phases_wg_ms": phases} if phases else {}),
             # multi: the level loop plus the gather that writes hops / in-degrees / inbound rows
             # (with GS_MV_FUSED=1 the gather runs fused with consume, and its whole time is charged)
             "bfs_roofline": roofline(bp, fam["bfs"] + fam.get("gather", 0.0) + fam.get("gather_consume", 0.0), steps,

@@ -81,6 +81,9 @@ struct MvArgs {
   uint32_t* ingress_acc;
   uint32_t N, SP, ASZ, fanout, capin, s0, Sg, UB, BSC, BSF, nbc, nbf, TW, ORW, any_fail, gcap, gcap_c;
   uint32_t lane_c, wave_c, record;
+  unsigned long long* pclk;  // GS_PHASE_PROFILE: gather phase clocks at [12..15] (thread 0 of each workgroup)
+  uint32_t exp;  // GS_MV_EXP (timing experiments only): 1 = gather writes no inbound rows (breaks results)
+  uint32_t gh;  // gather: nodes with more records (all slots) take the wave path
   // nodes with per-pair state [vlo, vhi) (= fine bins [flo, flo + fno)); pair = slot * NP + node - vlo.
   // A node-range partition rank runs the whole BFS but keeps the records, counts and
   // egress of its own nodes only.
@@ -376,16 +379,9 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint2*
       if (live && GS_OOB(vl, nv, a.err, "multi record node")) vl = 0;
       if (live) atomicOr(&visL[vl], (uint32_t)(rec >> (UB + BSC)));
       const uint32_t fb = live && f0 + (vl >> a.BSF) - a.flo < a.fno ? vl >> a.BSF : 0xFFFFu;  // kept bins only
-      uint32_t pos = 0;
-      for (uint32_t k = 0; k < NF; ++k) {  // one LDS atomic per wave and fine bin
-        const uint64_t m = __ballot(fb == k);
-        if (!m) continue;
-        uint32_t base = 0;
-        const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
-        if (lane_id() == leader) base = atomicAdd(&fcur[k], (uint32_t)__popcll(m));
-        base = (uint32_t)__shfl((int)base, (int)leader);
-        if (fb == k) pos = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
-      }
+      // the record's place in its fine bin's run: one LDS atomic per lane (measured faster
+      // than one per wave and fine bin by ballots: 19.5-19.7 vs 21.2-24.5 us per launch at C4)
+      const uint32_t pos = fb != 0xFFFFu ? atomicAdd(&fcur[fb], 1u) : 0u;
       if (fb != 0xFFFFu) {
         const uint32_t fl = f0 + fb - a.flo;
         const size_t pp = (size_t)a.pused[fl] + pos;
@@ -550,6 +546,14 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, ui
                                   const MvCsr& L, Body body) {
   const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BSF = a.BSF, BP = 1u << BSF, BPm = BP - 1;
   const uint32_t um = (1u << UB) - 1;
+  unsigned long long tm = a.pclk && tid == 0 ? wall_clock64() : 0;
+  auto mark = [&](int ph) {
+    if (a.pclk && tid == 0) {
+      const unsigned long long now = wall_clock64();
+      atomicAdd(&a.pclk[ph], now - tm);
+      tm = now;
+    }
+  };
   uint32_t *rs = L.rs, *rp = L.rp, *cn = L.cn, *cur = L.cur, *ctl = L.ctl, *keys = L.keys, *msk = L.msk;
   const unsigned long long* pool = a.pool + (size_t)f * a.pcap;  // (f: local kept-bin index)
   for (uint32_t i = tid; i <= BP; i += MV_GT) cn[i] = 0;
@@ -597,6 +601,7 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, ui
     atomicAdd(&cn[(uint32_t)(pool[rs[lv] + (t - rp[lv])] >> UB) & BPm], 1u);
   }
   __syncthreads();
+  mark(12);
   const uint32_t E2 = mv_block_scan(cn, BP, ctl);
   if (tid == 0) cn[BP] = E2;
   __syncthreads();
@@ -605,10 +610,19 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, ui
   // later ranges re-read the pool), so they do not stay live across body
   auto range = [&](uint32_t lo) {
     if (tid == 0) {
-      uint32_t h = lo;
-      while (h < nv && cn[h + 1] - cn[lo] <= gcap) ++h;
+      // the largest h with cn[h] - cn[lo] <= gcap (cn is non-decreasing): usually the whole bin
+      uint32_t h = nv;
+      if (cn[nv] - cn[lo] > gcap) {
+        uint32_t l2 = lo, h2 = nv;  // cn[l2] - cn[lo] <= gcap < cn[h2] - cn[lo]
+        while (h2 - l2 > 1) {
+          const uint32_t mid = (l2 + h2) >> 1;
+          if (cn[mid] - cn[lo] <= gcap) l2 = mid; else h2 = mid;
+        }
+        h = l2;
+      }
       if (h == lo) { atomicOr(a.err, ERR_MV_CAP); h = nv; }  // one node beyond the LDS CSR
       ctl[15] = h;
+      ctl[14] = 0;  // body's heavy-node count (k_mv_gather)
     }
     __syncthreads();
     const uint32_t hi = ctl[15];
@@ -640,8 +654,10 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, ui
     if (p < gcap) { keys[p] = kc[j]; msk[p] = mc[j]; }
   }
   place_pool(0, hi, MV_GC * MV_GT);
+  mark(13);
   body(0u, hi, 0u);
   __syncthreads();
+  mark(15);
   for (uint32_t lo = hi; lo < nv; lo = hi) {
     hi = range(lo);
     place_pool(lo, hi, 0);
@@ -723,18 +739,27 @@ __device__ inline uint32_t mv_pair_hop(const MvCsr& L, uint32_t r0, uint32_t r1,
 // API's gs_run_gossip, and gs_round unless GS_MV_FUSED=1). A lane appends its pair's
 // records as it finds them (rows of different lanes differ: measured faster than
 // filtering to a bitmap and storing row t of every lane together, 568 vs 697 us at C4).
+// A node with more than MV_GH records (all slots) is deferred to a whole wave: stake
+// weights make in-degrees power-law, and one such node in a wave of lanes held the
+// other 63 lanes for its whole list (every slot). (32; 4 under GS_FLAG_NARROW_WAVE_PATH)
 __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t f = mv_xcd_bin(blockIdx.x, a.fno);  // local kept-bin index
   if (f >= a.fno) return;
-  const uint32_t tid = threadIdx.x, BP = 1u << a.BSF, Sg = a.Sg, v0 = (a.flo + f) << a.BSF;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, BP = 1u << a.BSF, Sg = a.Sg, v0 = (a.flo + f) << a.BSF;
   if (v0 >= a.vhi) return;
   const uint32_t nv = min(BP, a.vhi - v0), gcap = a.gcap;
   const MvCsr L = mv_csr_lds(smem, BP, gcap);
   bool over = false;
   mv_bin_csr(a, f, nlev, nv, gcap, L, [&](uint32_t lo, uint32_t hi, uint32_t base) {
+    const unsigned long long tb = a.pclk && tid == 0 ? wall_clock64() : 0;
+    uint32_t* hvl = L.cur;  // the placement cursors are dead here: the heavy-node list
     for (uint32_t i = lo + tid; i < hi; i += MV_GT) {
       const uint32_t v = v0 + i, r0 = L.cn[i] - base, r1 = min(L.cn[i + 1] - base, gcap);
+      if (r1 - r0 > a.gh) {
+        hvl[atomicAdd(&L.ctl[14], 1u)] = i;
+        continue;
+      }
       for (uint32_t j = 0; j < Sg; ++j) {
         const size_t p = (size_t)(a.s0 + j) * a.NP + (v - a.vlo);
         uint32_t cc = 0, mh = 0xFFu;
@@ -745,7 +770,7 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             if (r + t >= r1 || !((m[t] >> j) & 1u)) continue;
-            if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = k[t];
+            if (cc < a.capin && !(a.exp & 1)) a.inb[(size_t)cc * a.PAIRS + p] = k[t];
             mh = min(mh, k[t] >> 24);
             ++cc;
           }
@@ -753,6 +778,36 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
         over |= cc > a.capin;
         a.cnt[p] = cc;
         a.hops[p] = (uint8_t)(v == L.sorg[j] ? 0u : (cc ? mh : 0xFFu));
+      }
+    }
+    __syncthreads();
+    if (a.pclk && tid == 0) atomicAdd(&a.pclk[14], wall_clock64() - tb);  // the light part ([15]: whole body)
+    // heavy nodes, one per wave: 64 records per step, each slot's ranks by ballot
+    const uint32_t nh = L.ctl[14];
+    for (uint32_t h = tid >> 6; h < nh; h += MV_GT / 64) {
+      const uint32_t i = hvl[h];
+      const uint32_t v = v0 + i, r0 = L.cn[i] - base, r1 = min(L.cn[i + 1] - base, gcap);
+      for (uint32_t j = 0; j < Sg; ++j) {
+        const size_t p = (size_t)(a.s0 + j) * a.NP + (v - a.vlo);
+        uint32_t cc = 0, mh = 0xFFu;
+        for (uint32_t rb = r0; rb < r1; rb += 64) {
+          const uint32_t r = rb + lane;
+          const bool b = r < r1 && ((L.msk[r] >> j) & 1u);
+          const uint32_t k = b ? L.keys[r] : 0xFFFFFFFFu;
+          const uint64_t bal = __ballot(b);
+          const uint32_t pos =
+              cc + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          if (b && pos < a.capin) a.inb[(size_t)pos * a.PAIRS + p] = k;
+          mh = min(mh, k >> 24);
+          cc += (uint32_t)__popcll(bal);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mh = min(mh, (uint32_t)__shfl_xor((int)mh, off));
+        if (lane == 0) {
+          over |= cc > a.capin;
+          a.cnt[p] = cc;
+          a.hops[p] = (uint8_t)(v == L.sorg[j] ? 0u : (cc ? mh : 0xFFu));
+        }
       }
     }
   });
@@ -906,7 +961,8 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   (void)ASZP;
   g.UB = std::max(1u, ceil_log2(N));
   g.BSC = std::min(13u, std::max(6u, g.UB > 8 ? g.UB - 8 : 0u));   // ~256 coarse bins
-  g.BSF = std::min(g.BSC, 10u);                                     // fine bins of <= 1,024 nodes
+  g.BSF = std::min(g.BSC, 9u);  // fine bins of <= 512 nodes (gather at C4: 301 vs 412 us with 1,024)
+  if (const char* x = std::getenv("GS_MV_BSF")) g.BSF = std::min(g.BSC, std::max(6u, (uint32_t)std::strtoul(x, nullptr, 10)));
   g.nbc = (N + (1u << g.BSC) - 1) >> g.BSC;
   g.nbf = g.nbc << (g.BSC - g.BSF);
   g.GW = std::min(28u, (64u - g.UB - g.BSC) & ~3u);
@@ -1010,6 +1066,10 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   const bool narrow = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) != 0;  // small tests reach every consume path
   a.lane_c = narrow ? 4u : 16u;
   a.wave_c = narrow ? 8u : 64u;
+  a.gh = narrow ? 4u : 32u;
+  a.pclk = e.phase_clk;
+  a.exp = 0;
+  if (const char* x = std::getenv("GS_MV_EXP")) a.exp = (uint32_t)std::strtoul(x, nullptr, 10);
   a.record = 0;
   a.PAIRS = e.PAIRS; a.area_cap = e.mv.area_cap; a.rows_cap = e.mv.rows_cap; a.q_cap = e.mv.q_cap;
   a.pcap = e.mv.pcap;

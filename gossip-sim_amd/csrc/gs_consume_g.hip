@@ -10,7 +10,7 @@
 //   received_cache.rs:38-63,100-131) for the entries that reached 20 upserts, found
 //   by a scan of the meta words: the (score, stake) order as one 31-bit key per entry sorted in registers,
 //   pre-add cumulative stake, prune bits set in the prunees' masks.
-// In-degree > 16 (consume) or entries > 16 keys (prune) are taken by the whole wave,
+// In-degree > 16 (consume) or entries > 32 keys (prune) are taken by the whole wave,
 // one pair at a time, after the wave's lanes finish their own pairs; in-degree > 64 by
 // an ordered single-lane selection. Results are identical to the generic per-pair code
 // in gs_kernels.hip (cp_generic), which remains the step-wise gs_consume_messages /
@@ -28,13 +28,14 @@ namespace {
 constexpr uint32_t CG_THREADS = 256;
 constexpr uint32_t CG_WAVES = CG_THREADS / 64;
 constexpr uint32_t CG_SCR = 128;  // per-wave LDS scratch (u32)
-constexpr uint32_t LANE_L = 16;  // register prune path capacity
+constexpr uint32_t LANE_L = 32;  // register prune path capacity (a prune wave's entries mostly hold 17-32 keys)
 
 struct CgArgs {
   const uint64_t* stake;
   const uint8_t* bucket;
   const uint32_t* peers;
   const uint16_t* hl;
+  const uint32_t* own;  // own-bucket rows (BINNED / MULTI; else null), ORW words each
   const uint32_t* origin;
   const uint8_t* obkt;
   const uint32_t* min_ingress;
@@ -52,7 +53,7 @@ struct CgArgs {
   uint32_t* ingress_acc;
   uint32_t* prune_acc;
   uint32_t* err;
-  uint32_t N, S, ASZ, capin;
+  uint32_t N, S, ASZ, capin, ORW;
   uint32_t NP, vlo;  // pair q = slot * NP + (node - vlo)
   size_t mso, msu;  // prune-mask strides of (slot, node)
   uint32_t lane_c, lane_l, wave_c;  // register-path bounds (16, 16) and wave-consume bound (64);
@@ -114,11 +115,18 @@ __device__ inline void after_consume(const CgArgs& a, uint32_t q, uint32_t meta,
 // PushActiveSet::prune (push_active_set.rs:56-71,143-151) for (prunee u, pruner v) of slot o.
 template <int ASZP>
 __device__ inline void apply_prune(const CgArgs& a, uint32_t o, uint32_t ob, uint32_t u, uint32_t v) {
-  const uint32_t ent = u * NB + min((uint32_t)a.bucket[u], ob);
-  const uint32_t hv = a.hl[ent];
+  const uint32_t bu = a.bucket[u], k = min(bu, ob);
+  uint32_t row[ASZP], hv;
+  if (a.own && k == bu) {  // the own-bucket row (64 B, cache-resident) instead of the full table's
+    const uint32_t* orow = a.own + (size_t)u * a.ORW;
+    load_row<ASZP>(orow, row);
+    hv = orow[ASZP] & 0xFFFFu;
+  } else {
+    const uint32_t ent = u * NB + k;
+    hv = a.hl[ent];
+    load_row<ASZP>(a.peers + (size_t)ent * ASZP, row);
+  }
   const uint32_t head = hv & 0xFF, L = hv >> 8;
-  uint32_t row[ASZP];
-  load_row<ASZP>(a.peers + (size_t)ent * ASZP, row);
   uint32_t hit = 0;
 #pragma unroll
   for (int s = 0; s < ASZP; ++s) {
@@ -128,7 +136,7 @@ __device__ inline void apply_prune(const CgArgs& a, uint32_t o, uint32_t ob, uin
   if (hit) atomicOr(&a.mask[o * a.mso + u * a.msu], hit);
 }
 
-// ---- prune, register path (len <= 16) ----
+// ---- prune, register path (len <= 32) ----
 template <int ASZP>
 __device__ inline uint32_t prune_lane(const CgArgs& a, uint32_t q, uint32_t o, uint32_t v, uint32_t len) {
   const size_t PAIRS = a.PAIRS;
@@ -150,6 +158,7 @@ __device__ inline uint32_t prune_lane(const CgArgs& a, uint32_t q, uint32_t o, u
       sk[i] = (uint32_t)i < len ? (((0x7Fu - ck_score(sk[i])) << 24) | pr[i]) : 0xFFFFFFFFu;
   }
   if (wl <= 8) sort_net<8>(sk);
+  else if (wl <= 16) sort_net<16>(sk);
   else sort_net<LANE_L>(sk);
   // sorted_unstable_by_key(Reverse((score, stake))), ties by id; pre-add cumulative stake;
   // skip(min_ingress_nodes); skip_while(cum < min_ingress_stake)
@@ -184,7 +193,7 @@ __device__ inline uint32_t prune_lane(const CgArgs& a, uint32_t q, uint32_t o, u
   return npr;
 }
 
-// ---- prune, wave path (16 < len <= 96): two entries per lane ----
+// ---- prune, wave path (32 < len <= 96): two entries per lane ----
 template <int ASZP>
 __device__ inline uint32_t prune_wave(const CgArgs& a, uint32_t q, uint32_t o, uint32_t v, uint32_t len) {
   const size_t PAIRS = a.PAIRS;
@@ -334,6 +343,7 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
 hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume) {
   CgArgs a;
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
+  a.own = e.own; a.ORW = e.ORW;
   a.min_ingress = e.min_ingress; a.thr = e.thr; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake;
   a.cnt = e.cnt; a.inb = e.inb; a.cmeta = e.cmeta; a.ckey = e.ckey; a.prune_round = e.prune_round;
   a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc;

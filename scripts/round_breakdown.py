@@ -25,6 +25,7 @@ def main():
             cur = []
     sel = [x for rr in rounds[r0:r1] for x in rr]
     tot, cnt, prev, gap = collections.Counter(), collections.Counter(), None, 0.0
+    mx = collections.Counter()
     for r in sel:
         n = next((f for f in FAMILIES if f in r["Kernel_Name"]), r["Kernel_Name"][:40])
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
@@ -33,11 +34,12 @@ def main():
         prev = max(prev or 0, e)
         tot[n] += (e - s) / 1e3
         cnt[n] += 1
+        mx[n] = max(mx[n], (e - s) / 1e3)
     k = max(1, r1 - r0)
     wall = (int(sel[-1]["End_Timestamp"]) - int(sel[0]["Start_Timestamp"])) / 1e3 / k
     print(f"rounds {r0}..{r1 - 1}: wall {wall:.1f} us/round, idle gaps {gap / k:.1f} us/round")
     for n, t in tot.most_common():
-        print(f"  {n:28s} {t / k:9.1f} us/round  {cnt[n] / k:6.1f} launches/round  {t / cnt[n]:8.1f} us/launch")
+        print(f"  {n:28s} {t / k:9.1f} us/round  {cnt[n] / k:6.1f} launches/round  {t / cnt[n]:8.1f} us/launch  max {mx[n]:8.1f}")
 
 
 if __name__ == "__main__":
