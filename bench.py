@@ -188,6 +188,7 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
             "bfs_mode": mode, "rounds": [warmup, warmup + steps], "ms_per_step": dt / steps * 1e3,
             "edges_per_s": E / dt, "origin_rounds_per_s": S * steps / dt,
             "pushes_per_origin_round": E / (S * steps),
+            "prunes_per_round_max": int(summ["prunes"].astype("int64").sum(axis=1).max()),
             "us_per_round": {k: round(v * 1e3 / steps, 1) for k, v in fam.items()},
             **({"gather_phases_wg_ms": phases} if phases else {}),
             # multi: the level loop plus the gather that writes hops / in-degrees / inbound rows

@@ -741,7 +741,7 @@ __device__ inline uint32_t mv_pair_hop(const MvCsr& L, uint32_t r0, uint32_t r1,
 // filtering to a bitmap and storing row t of every lane together, 568 vs 697 us at C4).
 // A node with more than MV_GH records (all slots) is deferred to a whole wave: stake
 // weights make in-degrees power-law, and one such node in a wave of lanes held the
-// other 63 lanes for its whole list (every slot). (32; 4 under GS_FLAG_NARROW_WAVE_PATH)
+// other 63 lanes for its whole list (every slot). (256; 4 under GS_FLAG_NARROW_WAVE_PATH)
 __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t f = mv_xcd_bin(blockIdx.x, a.fno);  // local kept-bin index
@@ -1066,7 +1066,8 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   const bool narrow = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) != 0;  // small tests reach every consume path
   a.lane_c = narrow ? 4u : 16u;
   a.wave_c = narrow ? 8u : 64u;
-  a.gh = narrow ? 4u : 32u;
+  a.gh = narrow ? 4u : 256u;  // C4: 291 us with no wave path, 311 at 32
+  if (const char* x = std::getenv("GS_MV_GH")) a.gh = (uint32_t)std::strtoul(x, nullptr, 10);
   a.pclk = e.phase_clk;
   a.exp = 0;
   if (const char* x = std::getenv("GS_MV_EXP")) a.exp = (uint32_t)std::strtoul(x, nullptr, 10);

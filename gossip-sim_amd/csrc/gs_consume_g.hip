@@ -28,7 +28,7 @@ namespace {
 constexpr uint32_t CG_THREADS = 256;
 constexpr uint32_t CG_WAVES = CG_THREADS / 64;
 constexpr uint32_t CG_SCR = 128;  // per-wave LDS scratch (u32)
-constexpr uint32_t LANE_L = 32;  // register prune path capacity (a prune wave's entries mostly hold 17-32 keys)
+constexpr uint32_t LANE_L = 16;  // register prune path capacity
 
 struct CgArgs {
   const uint64_t* stake;
@@ -43,6 +43,7 @@ struct CgArgs {
   const uint32_t* prank;
   const uint32_t* by_prank;
   const uint64_t* pstake;
+  const uint4* pinfo;  // by id: {prune rank, 0, stake lo, stake hi}
   const uint32_t* cnt;
   const uint32_t* inb;
   uint32_t* cmeta;
@@ -54,6 +55,7 @@ struct CgArgs {
   uint32_t* prune_acc;
   uint32_t* err;
   uint32_t N, S, ASZ, capin, ORW;
+  uint32_t exp;  // GS_CG_EXP (timing experiments only, breaks results): 1 = prunes not applied to masks
   uint32_t NP, vlo;  // pair q = slot * NP + (node - vlo)
   size_t mso, msu;  // prune-mask strides of (slot, node)
   uint32_t lane_c, lane_l, wave_c;  // register-path bounds (16, 16) and wave-consume bound (64);
@@ -133,62 +135,80 @@ __device__ inline void apply_prune(const CgArgs& a, uint32_t o, uint32_t ob, uin
     const uint32_t pos = (uint32_t)s >= head ? (uint32_t)s - head : (uint32_t)s + a.ASZ - head;
     hit |= (uint32_t)((uint32_t)s < a.ASZ && pos < L && row[s] == v) << s;
   }
-  if (hit) atomicOr(&a.mask[o * a.mso + u * a.msu], hit);
+  if (hit && !(a.exp & 1)) atomicOr(&a.mask[o * a.mso + u * a.msu], hit);
 }
 
 // ---- prune, register path (len <= 32) ----
+// Prunes found by a lane are appended (by ballot, in step order) to its wave's LDS list
+// (prunee id, pruner lane) and applied afterwards by all 64 lanes, one list entry each:
+// applied in place, a lane's prunes were one dependent row load after another, and
+// the wave waited for its longest entry's chain (a prune wave's 42 M prunes at C4).
+constexpr uint32_t CG_PL = 1024;  // per-wave deferred prunes (beyond: applied in place)
+struct PruneList {
+  uint32_t* u;
+  uint8_t* lane;
+  uint32_t n;  // wave-uniform among the lanes in the prune path
+};
+
 template <int ASZP>
-__device__ inline uint32_t prune_lane(const CgArgs& a, uint32_t q, uint32_t o, uint32_t v, uint32_t len) {
+__device__ inline uint32_t prune_lane(const CgArgs& a, uint32_t q, uint32_t o, uint32_t v, uint32_t len, PruneList& pl) {
   const size_t PAIRS = a.PAIRS;
   const uint32_t org = a.origin[o], ob = a.obkt[o], mi = a.min_ingress[o];
   const uint64_t sv = a.stake[v], so = a.stake[org];
   const uint64_t mis = min_ingress_stake(sv < so ? sv : so, a.thr[o]);
   const uint32_t wl = active_max<5>(len);
-  uint32_t sk[LANE_L];
-  {
+  // every entry's cache word, then its node's prune rank and stake (one 16-B load each,
+  // all in flight together)
+  uint32_t kk[LANE_L], nd[LANE_L];
+  uint64_t st[LANE_L];
 #pragma unroll
-    for (int i = 0; i < (int)LANE_L; ++i) sk[i] = (uint32_t)i < wl ? ntl(&(a.ckey + (size_t)i * PAIRS)[q]) : 0u;
-    asm volatile("" ::: "memory");
-    uint32_t pr[LANE_L];
+  for (int i = 0; i < (int)LANE_L; ++i) nd[i] = (uint32_t)i < wl ? ntl(&(a.ckey + (size_t)i * PAIRS)[q]) : 0u;
+  asm volatile("" ::: "memory");
 #pragma unroll
-    for (int i = 0; i < (int)LANE_L; ++i) pr[i] = (uint32_t)i < wl ? a.prank[(uint32_t)i < len ? ck_id(sk[i]) : 0u] : 0u;
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < (int)LANE_L; ++i)
-      sk[i] = (uint32_t)i < len ? (((0x7Fu - ck_score(sk[i])) << 24) | pr[i]) : 0xFFFFFFFFu;
-  }
-  if (wl <= 8) sort_net<8>(sk);
-  else if (wl <= 16) sort_net<16>(sk);
-  else sort_net<LANE_L>(sk);
-  // sorted_unstable_by_key(Reverse((score, stake))), ties by id; pre-add cumulative stake;
-  // skip(min_ingress_nodes); skip_while(cum < min_ingress_stake)
-  uint64_t cum = 0;
-  uint32_t npr = 0;
-  bool tail = false;
-#pragma unroll
-  for (int c0 = 0; c0 < (int)LANE_L; c0 += 8) {
-    if ((uint32_t)c0 >= wl) break;
-    uint32_t nd[8];
-    uint64_t st[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const uint32_t i = c0 + t, r = i < len ? sk[c0 + t] & 0xFFFFFFu : 0u;
-      nd[t] = a.by_prank[r];
-      st[t] = a.pstake[r];
+  for (int i = 0; i < (int)LANE_L; ++i) {
+    kk[i] = 0xFFFFFFFFu;
+    st[i] = 0;
+    if ((uint32_t)i < wl) {
+      const uint32_t id = (uint32_t)i < len ? ck_id(nd[i]) : 0u;
+      const uint4 x = a.pinfo[id];
+      kk[i] = (uint32_t)i < len ? (((0x7Fu - ck_score(nd[i])) << 24) | x.x) : 0xFFFFFFFFu;
+      st[i] = ((uint64_t)x.w << 32) | x.z;
+      nd[i] = id;
     }
-    asm volatile("" ::: "memory");
+  }
+  // sorted_unstable_by_key(Reverse((score, stake))), ties by id: entry i's position is the
+  // number of smaller keys (keys are distinct), its pre-add cumulative stake the saturating
+  // sum of their stakes (order-free); skip(min_ingress_nodes), then skip_while(cum <
+  // min_ingress_stake): pruned iff position >= mi and cum >= mis (cum never decreases).
+  // The rows are rewritten in prune order with the pruned flag.
+  uint32_t npr = 0;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const uint32_t i = c0 + t;
-      if (i < len) {
-        tail = tail || (i >= mi && cum >= mis);
-        const bool pruned = tail && nd[t] != org;
-        npr += pruned;
-        (a.ckey + (size_t)i * PAIRS)[q] = ck_make(nd[t], (0x7Fu - (sk[c0 + t] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
-        if (pruned) apply_prune<ASZP>(a, o, ob, nd[t], v);
-        cum = sat_add(cum, st[t]);
+  for (int i = 0; i < (int)LANE_L; ++i) {
+    if ((uint32_t)i >= wl) break;
+    uint32_t rank = 0;
+    uint64_t cum = 0;
+#pragma unroll
+    for (int j = 0; j < (int)LANE_L; ++j) {
+      if ((uint32_t)j >= wl) break;
+      const bool lt = kk[j] < kk[i];
+      rank += lt ? 1u : 0u;
+      cum = sat_add(cum, lt ? st[j] : 0ull);
+    }
+    const bool live = (uint32_t)i < len;
+    const bool pruned = live && rank >= mi && cum >= mis && nd[i] != org;
+    if (live) (a.ckey + (size_t)rank * PAIRS)[q] = ck_make(nd[i], (0x7Fu - (kk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
+    npr += pruned ? 1u : 0u;
+    const uint64_t pb = __ballot(pruned);
+    if (pruned) {
+      const uint32_t k = pl.n + __builtin_amdgcn_mbcnt_hi((uint32_t)(pb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pb, 0u));
+      if (k < CG_PL) {
+        pl.u[k] = nd[i];
+        pl.lane[k] = (uint8_t)lane_id();
+      } else if (!(a.exp & 2)) {
+        apply_prune<ASZP>(a, o, ob, nd[i], v);
       }
     }
+    pl.n += (uint32_t)__popcll(pb);
   }
   return npr;
 }
@@ -252,18 +272,26 @@ __device__ inline void finish_prune(const CgArgs& a, uint32_t q, uint32_t len, u
   if (npr && a.record) a.prune_acc[q] += npr;
 }
 
-// Adds each lane's prunee count to its slot's total: one atomic per wave when the
-// wave's pairs share a slot (consecutive pairs do), else one per lane. A per-pair
-// atomic on S counters serializes a prune round (all pairs of a slot hit one word).
-__device__ inline void add_slot_prunes(const CgArgs& a, uint32_t o, uint32_t npr) {
+// Adds each lane's prunee count to its slot's total. A block takes a contiguous range of
+// pairs, which spans few slots: the counts go to LDS counters (one per slot of the
+// range, sc[o - o_lo]) and each block adds them to the S global counters once at its
+// end. (S counters share a line or two: a global atomic per wave and slot made a prune
+// wave's 200 K atomics at C4 queue on one line, 2.4 of its 4.2 ms.) Slots beyond the
+// LDS counters (ranges of tiny slots) add per wave.
+constexpr uint32_t CG_SC = 64;
+__device__ inline void add_slot_prunes(const CgArgs& a, uint32_t o, uint32_t npr, uint32_t o_lo, uint32_t* sc) {
   const uint32_t o0 = __builtin_amdgcn_readfirstlane(o);
   if (__ballot(o != o0) == 0) {
     uint32_t s = npr;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
-    if (lane_id() == 0 && s) atomicAdd(&a.slot_prunes[o0], s);
+    if (lane_id() == 0 && s) {
+      if (o0 - o_lo < CG_SC) atomicAdd(&sc[o0 - o_lo], s);
+      else atomicAdd(&a.slot_prunes[o0], s);
+    }
   } else if (npr) {
-    atomicAdd(&a.slot_prunes[o], npr);
+    if (o - o_lo < CG_SC) atomicAdd(&sc[o - o_lo], npr);
+    else atomicAdd(&a.slot_prunes[o], npr);
   }
 }
 
@@ -308,19 +336,45 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_consume(CgArgs a) {
 // upserts (a scan of the meta words: no contended worklist counter).
 template <int ASZP>
 __global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
+  __shared__ uint32_t pl_u_all[CG_WAVES * CG_PL];
+  __shared__ uint8_t pl_l_all[CG_WAVES * CG_PL];
+  __shared__ uint32_t sc[CG_SC];  // prunes per slot of this block's range
+  const uint32_t wid = threadIdx.x >> 6;
   const uint32_t P = (uint32_t)a.PAIRS;
-  for (uint32_t p0 = blockIdx.x * CG_THREADS; p0 < P; p0 += gridDim.x * CG_THREADS) {
+  // this block's contiguous range of pairs (whole blocks of CG_THREADS)
+  const uint32_t nblk = (P + CG_THREADS - 1) / CG_THREADS, per = (nblk + gridDim.x - 1) / gridDim.x;
+  const uint32_t lo = min(P, blockIdx.x * per * CG_THREADS), hi = min(P, lo + per * CG_THREADS);
+  const uint32_t o_lo = lo / a.NP;
+  if (threadIdx.x < CG_SC) sc[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t p0 = lo; p0 < hi; p0 += CG_THREADS) {
     const uint32_t q = p0 + threadIdx.x;
-    const uint32_t meta = q < P ? ntl(&a.cmeta[q]) : 0u;
-    const bool due = q < P && ((meta >> 8) & 0xFF) >= MIN_NUM_UPSERTS;
+    const uint32_t meta = q < hi ? ntl(&a.cmeta[q]) : 0u;
+    const bool due = q < hi && ((meta >> 8) & 0xFF) >= MIN_NUM_UPSERTS;
     if (!__ballot(due)) continue;
     const uint32_t o = q / a.NP, v = a.vlo + (q - o * a.NP);
     const uint32_t len = meta & 0xFF;
     const bool heavy = due && len > a.lane_l;
     uint32_t npr = 0;
+    PruneList pl{pl_u_all + wid * CG_PL, pl_l_all + wid * CG_PL, 0u};
     if (due && !heavy) {
-      npr = prune_lane<ASZP>(a, q, o, v, len);
+      npr = prune_lane<ASZP>(a, q, o, v, len, pl);
       finish_prune(a, q, len, npr);
+    }
+    uint32_t pn = pl.n;  // (0 in lanes outside the lane path)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) pn = max(pn, (uint32_t)__shfl_xor((int)pn, off));
+    pn = min(pn, CG_PL);
+    if (pn) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t qb = p0 + (wid << 6);
+      for (uint32_t k = lane_id(); k < pn; k += 64) {
+        const uint32_t pq = qb + pl.lane[k];
+        const uint32_t po = pq / a.NP;
+        if (!(a.exp & 2)) apply_prune<ASZP>(a, po, a.obkt[po], pl.u[k], a.vlo + (pq - po * a.NP));
+      }
+      __builtin_amdgcn_wave_barrier();  // the list is reused by the wave's next pairs
     }
     uint64_t hv = __ballot(heavy);
     while (hv) {  // the wave's long entries, one at a time
@@ -333,8 +387,10 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
       if (lane_id() == 0) finish_prune(a, hq, hlen, hn);
       if ((int)lane_id() == l) npr = hn;
     }
-    add_slot_prunes(a, o, npr);
+    add_slot_prunes(a, o, npr, o_lo, sc);
   }
+  __syncthreads();
+  if (threadIdx.x < CG_SC && sc[threadIdx.x]) atomicAdd(&a.slot_prunes[o_lo + threadIdx.x], sc[threadIdx.x]);
 }
 
 }  // namespace
@@ -344,7 +400,9 @@ hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume) {
   CgArgs a;
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
   a.own = e.own; a.ORW = e.ORW;
-  a.min_ingress = e.min_ingress; a.thr = e.thr; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake;
+  a.exp = 0;
+  if (const char* x = std::getenv("GS_CG_EXP")) a.exp = (uint32_t)std::strtoul(x, nullptr, 10);
+  a.min_ingress = e.min_ingress; a.thr = e.thr; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake; a.pinfo = e.pinfo;
   a.cnt = e.cnt; a.inb = e.inb; a.cmeta = e.cmeta; a.ckey = e.ckey; a.prune_round = e.prune_round;
   a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc;
   a.NP = e.NP; a.vlo = e.vlo;

@@ -71,6 +71,7 @@ struct Engine {
   uint32_t* prank = nullptr;     // rank by (stake desc, id asc): prune-order key
   uint32_t* by_prank = nullptr;
   uint64_t* pstake = nullptr;    // stake by prune rank
+  uint4* pinfo = nullptr;        // by node id: {prune rank, 0, stake lo, stake hi} (one load per cache key)
   // slot arrays
   uint32_t* origin = nullptr;
   uint8_t* obkt = nullptr;
