@@ -833,7 +833,13 @@ __device__ void block_kth_bits(const uint32_t* __restrict__ bm, uint32_t W, cons
   const uint32_t chunk = (W + T - 1) / T;
   const uint32_t lo = min(W, t * chunk), hi = min(W, lo + chunk);
   uint32_t c = 0;
-  for (uint32_t i = lo; i < hi; ++i) c += __popc(bm[i]);
+  for (uint32_t i = lo; i < hi; i += 8) {  // 8 loads in flight per wait (a slot's bitmap is N / 32 words)
+    uint32_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = i + j < hi ? bm[i + j] : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c += __popc(x[j]);
+  }
   const uint32_t incl = wave_incl_scan(c);
   if ((t & 63) == 63) scratch[t >> 6] = incl;
   __syncthreads();
@@ -874,24 +880,60 @@ __global__ __launch_bounds__(1024) void k_stats_finalize(StatsArgs a, uint32_t r
   s.stranded = a.rs_u32[o * 4 + 2];
   s.prunes = a.slot_prunes[o];
   s.stranded_stake_sum = a.rs_ssum[o];
-  // HopsStat over reached non-origin nodes (hops 1..254)
-  uint32_t count = 0;
-  uint64_t hsum = 0;
-  for (uint32_t i = 1; i < 255; ++i) { count += hb[i]; hsum += (uint64_t)i * hb[i]; }
-  s.hop_count = count;
-  s.hop_sum = hsum;
-  if (count) {
-    const uint32_t klo = count % 2 ? count / 2 : count / 2 - 1, khi = count / 2;
-    uint32_t run = 0;
-    bool got_min = false;
-    for (uint32_t i = 1; i < 255; ++i) {
-      if (!hb[i]) continue;
-      if (!got_min) { s.hop_min = i; got_min = true; }
-      s.hop_max = i;
-      if (klo >= run && klo < run + hb[i]) s.hop_med_lo = i;
-      if (khi >= run && khi < run + hb[i]) s.hop_med_hi = i;
-      run += hb[i];
+  // HopsStat over reached non-origin nodes (hops 1..254), by wave 0: four bins per lane,
+  // a wave scan of the counts, min/max from ballots, the medians from the scan
+  __shared__ uint32_t hs[6];  // count, min, max, med lo, med hi, (pad)
+  __shared__ unsigned long long hsum_s;
+  if (threadIdx.x < 64) {
+    const uint32_t l = threadIdx.x;
+    uint32_t h[4], c = 0;
+    uint64_t sm = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint32_t i = 4 * l + t;
+      h[t] = (i >= 1 && i < 255) ? hb[i] : 0u;
+      c += h[t];
+      sm += (uint64_t)i * h[t];
     }
+    const uint32_t incl = wave_incl_scan(c);
+    const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)sm, off), hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(sm >> 32), off);
+      sm += ((uint64_t)hi32 << 32) | lo32;
+    }
+    const uint64_t nz = __ballot(c > 0);
+    if (l == 0) { hs[0] = total; hsum_s = sm; }
+    if (total) {
+      const uint32_t before = incl - c;
+      if (l == (uint32_t)(__ffsll((long long)nz) - 1))
+        for (int t = 0; t < 4; ++t)
+          if (h[t]) { hs[1] = 4 * l + t; break; }
+      if (l == 63u - (uint32_t)__clzll((long long)nz))
+        for (int t = 3; t >= 0; --t)
+          if (h[t]) { hs[2] = 4 * l + t; break; }
+      const uint32_t ks[2] = {total % 2 ? total / 2 : total / 2 - 1, total / 2};
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (ks[q] >= before && ks[q] < incl) {
+          uint32_t run = before;
+          for (int t = 0; t < 4; ++t) {
+            if (ks[q] < run + h[t]) { hs[3 + q] = 4 * l + t; break; }
+            run += h[t];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t count = hs[0];
+  s.hop_count = count;
+  s.hop_sum = hsum_s;
+  if (count) {
+    s.hop_min = hs[1];
+    s.hop_max = hs[2];
+    s.hop_med_lo = hs[3];
+    s.hop_med_hi = hs[4];
   }
   const uint32_t* bmo = a.bm + (size_t)o * a.W;
   const uint32_t sc = s.stranded;
