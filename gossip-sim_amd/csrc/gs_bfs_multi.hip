@@ -1126,6 +1126,11 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
   volatile uint32_t* hl = e.mv_hlvl;  // host-mapped: expand(d) writes lvl[d]
   volatile uint32_t* hs = e.mv_hlvl + 256;  // host-mapped: the small-level kernel's (level, entries)
   const size_t lds_s = (size_t)fno * 4;
+  // the host enqueues level d after seeing level d - lag's frontier size (levels past the
+  // end run as no-ops); a short lag left the GPU idle for the host's reaction at every
+  // short tail level
+  uint32_t lag = 2;
+  if (const char* x = std::getenv("GS_MV_LAG")) lag = std::max<uint32_t>(1, (uint32_t)std::strtoul(x, nullptr, 10));
   for (uint32_t g = 0; g < (uint32_t)e.mv_groups.size(); ++g) {
     const MvGroup& gr = e.mv_groups[g];
     MvArgs a = mv_args(e, gr, g);
@@ -1155,9 +1160,9 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
         GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, d,
                                                     e.mv_q[d & 1]));
         hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, d, e.mv_q[(d + 1) & 1]);
-        if (d >= dl + 2) {
+        if (d >= dl + lag) {
           uint32_t x = 0;
-          if ((r = mv_wait(hl + (d - 2), e.st, x))) return r;
+          if ((r = mv_wait(hl + (d - lag), e.st, x))) return r;
           if (x == 0) { nlev = d + 1; done = true; break; }
           if (x <= a.small) { ++d; break; }  // levels d - 1, d are enqueued; small levels from d + 1
         }

@@ -33,7 +33,9 @@ hipEvent_t Engine::ev_take() {
     x = ev_pool.back();
     ev_pool.pop_back();
   } else {
-    hipEventCreate(&x);
+    // timing only (read after a stream sync): no system-scope fence -- its L2 write-back
+    // idled the GPU ~10 us at every recorded family boundary
+    hipEventCreateWithFlags(&x, hipEventDisableSystemFence);
   }
   return x;
 }
