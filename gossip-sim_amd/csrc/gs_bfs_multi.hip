@@ -434,6 +434,7 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint2*
 
 // ------------------------------------------------------------ small levels ----
 constexpr uint32_t MV_ST = 1024;     // threads of the small-level workgroup
+constexpr uint32_t MV_SMALL_LP = 8192;  // fine bins up to which the small kernel keeps pool fills in LDS
 constexpr uint32_t MV_SMALL = 1024;  // frontier entries at most for a small level (default; GS_MV_SMALL): C4 917 us vs 936 at 4096
 
 template <class T>
@@ -451,19 +452,26 @@ __device__ inline T mv_ld(T* p) {  // device-scope load: lines updated by atomic
 template <int ASZP>
 __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2* __restrict__ q0,
                                                     uint2* __restrict__ q1, uint32_t* __restrict__ hstate) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t snap[];  // [fno] pool fill at level start
+  // [fno] pool fill at level start, then (when LP) [fno] the running fill: the records'
+  // pool places come from LDS atomics, the global fills are written once at the end
+  extern __shared__ __attribute__((aligned(16))) uint32_t snap[];
   __shared__ uint32_t sorg[32], sfk[32], gt[GT_WORDS], cnt_s;
   const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BPm = (1u << BSC) - 1;
+  const bool LP = a.fno <= MV_SMALL_LP;  // (uniform)
+  uint32_t* lp = snap + a.fno;
   if (tid < a.Sg) {
     sorg[tid] = a.origin[a.s0 + tid];
     sfk[tid] = a.fk[a.s0 + tid];
   }
   for (uint32_t i = tid; i < GT_WORDS; i += MV_ST) gt[i] = a.gt[i];
+  for (uint32_t f = tid; f < a.fno; f += MV_ST) {
+    snap[f] = mv_ld(&a.pused[f]);
+    if (LP) lp[f] = snap[f];
+  }
   uint32_t d = d0, qn = a.lvl[d0];
   while (qn > 0 && qn <= a.small && d < 254) {
     uint2* qcur = (d & 1) ? q1 : q0;
     uint2* qnxt = (d & 1) ? q0 : q1;
-    for (uint32_t f = tid; f < a.fno; f += MV_ST) snap[f] = mv_ld(&a.pused[f]);
     if (tid == 0) {
       cnt_s = 0;
       __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -475,15 +483,19 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
       if (i < qn) mv_expand_entry<ASZP>(a, qcur[i], sorg, sfk, row, acc, u);
-      // every atomic of the entry is issued before any result is used (one wait, not
-      // one round trip per pushed-to peer)
-      uint32_t old[ASZP], pp[ASZP];
+      // every global access of the entry is issued before any result is used (one wait,
+      // not one round trip per pushed-to peer): the vis atomics, the peers' buckets and,
+      // without LDS fills, the pool-place atomics
+      uint32_t old[ASZP], pp[ASZP], bw[ASZP];
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) old[s] = acc[s] ? atomicOr(&a.vis[row[s]], acc[s]) : 0xFFFFFFFFu;
 #pragma unroll
+      for (int s = 0; s < ASZP; ++s) bw[s] = acc[s] ? (uint32_t)a.bucket[row[s]] : 0u;
+#pragma unroll
       for (int s = 0; s < ASZP; ++s) {
         const uint32_t f = (row[s] >> a.BSF) - a.flo;
-        pp[s] = acc[s] && f < a.fno ? atomicAdd(&a.pused[f], 1u) : 0xFFFFFFFFu;  // kept bins only
+        const bool kept = acc[s] && f < a.fno;  // kept bins only
+        pp[s] = !kept ? 0xFFFFFFFFu : LP ? atomicAdd(&lp[f], 1u) : atomicAdd(&a.pused[f], 1u);
       }
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) {
@@ -499,22 +511,26 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2
             atomicOr(a.err, ERR_MV_CAP);
         }
         if (nw) {  // this thread's first arrivals at w (another thread may add more bits to w)
-          const uint32_t bw = a.bucket[w];
-          const uint32_t n = mv_parts(gt, w, nw, bw, nullptr, 0);
+          const uint32_t n = mv_parts(gt, w, nw, bw[s], nullptr, 0);
           const uint32_t base = atomicAdd(&cnt_s, n);
-          if ((size_t)base + n <= a.q_cap) mv_parts(gt, w, nw, bw, qnxt, base);
+          if ((size_t)base + n <= a.q_cap) mv_parts(gt, w, nw, bw[s], qnxt, base);
           else atomicOr(a.err, ERR_MV_CAP);
         }
       }
     }
     __syncthreads();
-    for (uint32_t f = tid; f < a.fno; f += MV_ST)  // the level's pool run of every kept fine bin
-      a.Lt[(size_t)d * a.fno + f] = make_uint2(snap[f], mv_ld(&a.pused[f]) - snap[f]);
+    for (uint32_t f = tid; f < a.fno; f += MV_ST) {  // the level's pool run of every kept fine bin
+      const uint32_t now = LP ? lp[f] : mv_ld(&a.pused[f]);
+      a.Lt[(size_t)d * a.fno + f] = make_uint2(snap[f], now - snap[f]);
+      snap[f] = now;
+    }
     qn = min(cnt_s, (uint32_t)a.q_cap);
     ++d;
     if (tid == 0) a.lvl[d] = qn;
     __syncthreads();
   }
+  if (LP)
+    for (uint32_t f = tid; f < a.fno; f += MV_ST) a.pused[f] = lp[f];
   if (tid == 0) {
     __hip_atomic_store(&hstate[1], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&hstate[0], d, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // the host polls this word
@@ -1114,7 +1130,7 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       return r;
     GS_ASZP_DISPATCH(e.ASZP, {
       r = hipFuncSetAttribute((const void*)k_mv_small<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(mv_kept_bins(e) * 4));
+                              (int)(mv_kept_bins(e) * (mv_kept_bins(e) <= MV_SMALL_LP ? 8 : 4)));
     });
     if (r != hipSuccess) return r;
     e.mv_attr_set = true;
@@ -1125,7 +1141,7 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
   const uint32_t xgrid = 2048;
   volatile uint32_t* hl = e.mv_hlvl;  // host-mapped: expand(d) writes lvl[d]
   volatile uint32_t* hs = e.mv_hlvl + 256;  // host-mapped: the small-level kernel's (level, entries)
-  const size_t lds_s = (size_t)fno * 4;
+  const size_t lds_s = (size_t)fno * (fno <= MV_SMALL_LP ? 8 : 4);
   // the host enqueues level d after seeing level d - lag's frontier size (levels past the
   // end run as no-ops); a short lag left the GPU idle for the host's reaction at every
   // short tail level
