@@ -150,6 +150,43 @@ struct PruneList {
   uint32_t n;  // wave-uniform among the lanes in the prune path
 };
 
+// Entries [0, W) of a lane's cache entry (keys ~0 beyond its length): each entry's position
+// in prune order = the number of smaller keys (keys are distinct), its pre-add cumulative
+// stake = the saturating sum of their stakes (order-free); the rows are rewritten in prune
+// order with the pruned flag, prunes are appended to the wave's list.
+template <int ASZP, int W>
+__device__ inline void prune_ranks(const CgArgs& a, uint32_t q, uint32_t o, uint32_t ob, uint32_t org, uint32_t v,
+                                   uint32_t len, uint32_t mi, uint64_t mis, const uint32_t (&kk)[LANE_L],
+                                   const uint32_t (&nd)[LANE_L], const uint64_t (&st)[LANE_L], PruneList& pl,
+                                   uint32_t& npr) {
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    uint32_t rank = 0;
+    uint64_t cum = 0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const bool lt = kk[j] < kk[i];
+      rank += lt ? 1u : 0u;
+      cum = sat_add(cum, lt ? st[j] : 0ull);
+    }
+    const bool live = (uint32_t)i < len;
+    const bool pruned = live && rank >= mi && cum >= mis && nd[i] != org;
+    if (live) (a.ckey + (size_t)rank * a.PAIRS)[q] = ck_make(nd[i], (0x7Fu - (kk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
+    npr += pruned ? 1u : 0u;
+    const uint64_t pb = __ballot(pruned);
+    if (pruned) {
+      const uint32_t k = pl.n + __builtin_amdgcn_mbcnt_hi((uint32_t)(pb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pb, 0u));
+      if (k < CG_PL) {
+        pl.u[k] = nd[i];
+        pl.lane[k] = (uint8_t)lane_id();
+      } else if (!(a.exp & 2)) {
+        apply_prune<ASZP>(a, o, ob, nd[i], v);
+      }
+    }
+    pl.n += (uint32_t)__popcll(pb);
+  }
+}
+
 template <int ASZP>
 __device__ inline uint32_t prune_lane(const CgArgs& a, uint32_t q, uint32_t o, uint32_t v, uint32_t len, PruneList& pl) {
   const size_t PAIRS = a.PAIRS;
@@ -182,34 +219,8 @@ __device__ inline uint32_t prune_lane(const CgArgs& a, uint32_t q, uint32_t o, u
   // min_ingress_stake): pruned iff position >= mi and cum >= mis (cum never decreases).
   // The rows are rewritten in prune order with the pruned flag.
   uint32_t npr = 0;
-#pragma unroll
-  for (int i = 0; i < (int)LANE_L; ++i) {
-    if ((uint32_t)i >= wl) break;
-    uint32_t rank = 0;
-    uint64_t cum = 0;
-#pragma unroll
-    for (int j = 0; j < (int)LANE_L; ++j) {
-      if ((uint32_t)j >= wl) break;
-      const bool lt = kk[j] < kk[i];
-      rank += lt ? 1u : 0u;
-      cum = sat_add(cum, lt ? st[j] : 0ull);
-    }
-    const bool live = (uint32_t)i < len;
-    const bool pruned = live && rank >= mi && cum >= mis && nd[i] != org;
-    if (live) (a.ckey + (size_t)rank * PAIRS)[q] = ck_make(nd[i], (0x7Fu - (kk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
-    npr += pruned ? 1u : 0u;
-    const uint64_t pb = __ballot(pruned);
-    if (pruned) {
-      const uint32_t k = pl.n + __builtin_amdgcn_mbcnt_hi((uint32_t)(pb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pb, 0u));
-      if (k < CG_PL) {
-        pl.u[k] = nd[i];
-        pl.lane[k] = (uint8_t)lane_id();
-      } else if (!(a.exp & 2)) {
-        apply_prune<ASZP>(a, o, ob, nd[i], v);
-      }
-    }
-    pl.n += (uint32_t)__popcll(pb);
-  }
+  if (wl <= 8) prune_ranks<ASZP, 8>(a, q, o, ob, org, v, len, mi, mis, kk, nd, st, pl, npr);
+  else prune_ranks<ASZP, LANE_L>(a, q, o, ob, org, v, len, mi, mis, kk, nd, st, pl, npr);
   return npr;
 }
 

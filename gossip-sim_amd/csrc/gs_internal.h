@@ -137,6 +137,7 @@ struct Engine {
   bool rot_have_prev = false;
   uint32_t rot_parity = 0;          // parity of the last rotation's round
   size_t rwg_attr_lds = 0;          // dynamic LDS the round kernel was last configured for
+  bool rwg_attr_prof = false;       // ... and for which instantiation (phase clocks or not)
   // node-range partition (gs_partition.hip): this rank owns node ids [part_lo, part_hi)
   // (= [vlo, vlo + NP)) and the fine bins [part_flo, part_flo + part_fno) of the multi BFS
   bool part_on = false;

@@ -97,7 +97,7 @@ struct RoundArgs {
 // Phase clock: thread 0 adds the time since the last mark to phase_clk[ph].
 #define RWG_MARK(ph)                                                              \
   do {                                                                            \
-    if (a.phase_clk && tid == 0) {                                                \
+    if (PROF && a.phase_clk && tid == 0) {                                        \
       const unsigned long long now_ = wall_clock64();                             \
       atomicAdd(&a.phase_clk[ph], now_ - t_mark);                                 \
       t_mark = now_;                                                              \
@@ -601,7 +601,9 @@ __device__ inline void compact_push(const uint32_t (&row)[ASZP], uint32_t pushm,
   }
 }
 
-template <int ASZP, bool OFF16, int FP>
+// PROF: the phase clocks (GS_PHASE_PROFILE) are compiled in -- only for the C2 shape's
+// instantiation; their long-lived 64-bit clock state spilled to scratch in every build.
+template <int ASZP, bool OFF16, int FP, bool PROF>
 __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundArgs a) {
   using PMT = typename std::conditional<(ASZP <= 16), uint16_t, uint32_t>::type;
   using OFFT = typename std::conditional<OFF16, uint16_t, uint32_t>::type;
@@ -632,7 +634,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   const uint32_t org = a.origin[o], ob = a.obkt[o], nf = a.nfail[o];
   const size_t base = (size_t)o * N;
   uint32_t errf = 0;
-  unsigned long long t_mark = a.phase_clk && tid == 0 ? wall_clock64() : 0;
+  unsigned long long t_mark = PROF && a.phase_clk && tid == 0 ? wall_clock64() : 0;
 
   for (uint32_t i = tid; i < (N + 1) / 2; i += RWG_THREADS) cntw[i] = 0;
   for (uint32_t v = tid; v < N; v += RWG_THREADS) {
@@ -712,7 +714,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
     const uint32_t l3n = l3 == 2 ? 0 : l3 + 1, l3c = l3n == 2 ? 0 : l3n + 1;
     if (tid == 0) ctrl[C_LVL + l3c] = 0;
     uint16_t* nxt = cur + qn;
-    unsigned long long tl0 = (a.phase_clk && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long tl0 = (PROF && a.phase_clk && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
     for (uint32_t i0 = 0; i0 < qn; i0 += RWG_THREADS) {
       if (i0 + (wid << 6) >= qn) continue;  // wave-uniform: no frontier node for this wave
       const bool valid = i0 + tid < qn;
@@ -727,7 +729,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
 #pragma unroll
         for (int j = 0; j < FP; ++j)
           if ((uint32_t)j < kk) dst[j] = lst_l[u * fc + j];
-        if (a.phase_clk && tid == 0 && i0 == 0) {
+        if (PROF && a.phase_clk && tid == 0 && i0 == 0) {
           const unsigned long long t1 = __builtin_amdgcn_s_memtime();
           prof[0] += t1 - tl0;  // level start -> push list read (shader cycles)
           tl0 = t1;
@@ -767,26 +769,26 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
 #pragma unroll
       for (int j = 0; j < FP; ++j)
         if ((newm >> j) & 1u) nxt[idx++] = (uint16_t)dst[j];
-      if (a.phase_clk && tid == 0 && i0 == 0) {
+      if (PROF && a.phase_clk && tid == 0 && i0 == 0) {
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         prof[1] += t1 - tl0;  // row loaded -> pushes done
         tl0 = t1;
       }
     }
-    if (a.phase_clk && tid == 0) {
+    if (PROF && a.phase_clk && tid == 0) {
       const unsigned long long t1 = __builtin_amdgcn_s_memtime();
       prof[2] += t1 - tl0;  // remaining iterations of the level
       tl0 = t1;
     }
     __syncthreads();
     cur += qn;
-    if (a.phase_clk && tid == 0) {
+    if (PROF && a.phase_clk && tid == 0) {
       prof[4] += 1;  // levels
       prof[3] += __builtin_amdgcn_s_memtime() - tl0;  // the barrier
     }
   }
 
-  if (a.phase_clk && tid == 0) {
+  if (PROF && a.phase_clk && tid == 0) {
     atomicAdd(&a.phase_clk[8], prof[0]);
     atomicAdd(&a.phase_clk[9], prof[1]);
     atomicAdd(&a.phase_clk[10], prof[2]);
@@ -1027,16 +1029,25 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   RWG_MARK(6);
 }
 
-template <int ASZP, bool OFF16, int FP>
-static hipError_t launch_rwg_fp(Engine& e, const RoundArgs& a, size_t lds) {
-  if (e.rwg_attr_lds != lds) {
-    hipError_t r = hipFuncSetAttribute((const void*)k_round_wg<ASZP, OFF16, FP>,
+template <int ASZP, bool OFF16, int FP, bool PROF>
+static hipError_t launch_rwg_p(Engine& e, const RoundArgs& a, size_t lds) {
+  if (e.rwg_attr_lds != lds || e.rwg_attr_prof != PROF) {
+    hipError_t r = hipFuncSetAttribute((const void*)k_round_wg<ASZP, OFF16, FP, PROF>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (r != hipSuccess) return r;
     e.rwg_attr_lds = lds;
+    e.rwg_attr_prof = PROF;
   }
-  hipLaunchKernelGGL((k_round_wg<ASZP, OFF16, FP>), dim3(e.S), dim3(RWG_THREADS), lds, e.st, a);
+  hipLaunchKernelGGL((k_round_wg<ASZP, OFF16, FP, PROF>), dim3(e.S), dim3(RWG_THREADS), lds, e.st, a);
   return hipSuccess;
+}
+
+template <int ASZP, bool OFF16, int FP>
+static hipError_t launch_rwg_fp(Engine& e, const RoundArgs& a, size_t lds) {
+  if constexpr (ASZP == 12 && OFF16 && FP == 6) {  // C2's shape: phase clocks available
+    if (a.phase_clk) return launch_rwg_p<ASZP, OFF16, FP, true>(e, a, lds);
+  }
+  return launch_rwg_p<ASZP, OFF16, FP, false>(e, a, lds);
 }
 
 template <int ASZP, bool OFF16>
