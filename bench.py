@@ -37,6 +37,8 @@ Secondary legs at N = 1 (reported beside `value`, never part of it):
       fraction of HBM peak is the north-star figure.
   c3: BASELINE C3's per-GPU share -- 100k nodes, active-set-size sweep values 12
       and 20 (sims 0 and 8 of 16 dealt over 8 GPUs), one engine per value.
+  c5: BASELINE C5's 10M-node graph on one GPU (2 origin slots, one engine): the
+      propagation work each node-range partition rank repeats.
 """
 import argparse
 import glob
@@ -200,6 +202,48 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
                                      "B_prop (SURVEY 8d), summed over slots", f"bfs_{mode}_c4")}
 
 
+def c5_leg(gs, synth, args, nodes=10_000_000, slots=2, warmup=3, steps=10):
+    """BASELINE C5's graph on one GPU: a 10M-node network, origin ranks 1 and 2 as slots of
+    ONE engine (multi-source BFS). A node-range partition over K ranks divides the per-pair
+    state, but every rank runs this whole BFS, so this is the per-GPU
+    propagation work of C5."""
+    import numpy as np
+    stakes = synth.power_law_stakes(nodes)
+    order = np.argsort(-stakes.astype(np.float64), kind="stable")
+    origins = [int(order[0]), int(order[1])][:slots]
+    eng = gs.Engine(stakes, len(origins), fanout=args.fanout, active_set_size=args.active_set_size,
+                    rotation_probability=0.013333, seed=args.seed, device=0, profile=True, bfs_mode=args.large_mode)
+    eng.set_slots(origins, args.min_ingress, args.threshold)
+    t0 = time.perf_counter()
+    eng.init_active_sets()
+    eng.sync()
+    t_init = time.perf_counter() - t0
+    for r in range(warmup):
+        eng.round(r, record=False)
+    eng.sync()
+    eng.kernel_time_reset()
+    t0 = time.perf_counter()
+    for r in range(warmup, warmup + steps):
+        eng.round(r, record=True)
+    eng.sync()
+    dt = time.perf_counter() - t0
+    summ = eng.summaries()
+    E = float(summ["pushes"].astype("float64").sum())
+    V = float(summ["visited"].astype("float64").sum())
+    fam = {k: eng.kernel_time(k)[0] for k in ("bfs", "gather", "consume", "rotate", "stats")}
+    info = eng.info()
+    eng.close()
+    mode = {2: "level", 3: "binned", 4: "multi"}.get(info["bfs_mode"], str(info["bfs_mode"]))
+    return {"workload": f"C5 graph on one GPU: {nodes}-node power-law network, origin ranks 1-{len(origins)} as "
+                        f"slots of one engine (unpartitioned; every partition rank runs this BFS)",
+            "bfs_mode": mode, "rounds": [warmup, warmup + steps], "ms_per_step": dt / steps * 1e3,
+            "edges_per_s": E / dt, "init_active_sets_s": t_init,
+            "us_per_round": {k: round(v * 1e3 / steps, 1) for k, v in fam.items()},
+            "device_bytes": info["device_bytes"],
+            "bfs_roofline": roofline(b_prop(V, E, args.active_set_size), fam["bfs"] + fam["gather"], steps,
+                                     f"BFS ({mode})", "B_prop (SURVEY 8d), summed over slots")}
+
+
 def c3_leg(gs, synth, args, nodes=100_000, warmup=5, steps=20):
     """BASELINE C3's share of one GPU: ASZ 12 and 20 (sims 0 and 8 of the 16-sim sweep
     dealt over 8 GPUs), one engine (one slot) per value, origin rank 1."""
@@ -284,7 +328,7 @@ def main():
     import gossip_sim_amd.synth as synth
 
     if args.only_large:
-        legs = {"c4": c4_leg, "c3": c3_leg}
+        legs = {"c4": c4_leg, "c3": c3_leg, "c5": c5_leg}
         out = {k: legs[k](gs, synth, args) for k in args.legs.split(",")}
         print(json.dumps(out), flush=True)
         return
@@ -442,6 +486,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_large:
         out["c4"] = c4_leg(gs, synth, args)
         out["c3"] = c3_leg(gs, synth, args)
+        out["c5"] = c5_leg(gs, synth, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -493,6 +493,10 @@ __device__ inline uint32_t prune_wave(const RoundArgs& a, uint32_t* mkw, const u
   return npr;
 }
 
+// The slot's prune-stake threshold, loaded where a prune needs it (held in a register
+// across the whole consume phase it was spilled to scratch).
+__device__ inline double rwg_thr(const RoundArgs& a, uint32_t o) { return *(volatile const double*)&a.thr[o]; }
+
 // Finishes a node's cache step: prune when due (lane path), else clear the
 // previous round's pruned-len and record no prunes.
 __device__ inline void finish_node(const RoundArgs& a, size_t p, uint32_t meta, uint32_t len, uint32_t up,
@@ -881,7 +885,6 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
 
   // ---------------- C + D: consume, prune (register path) -------------------
   const uint32_t mi = a.min_ingress[o];
-  const double thr = a.thr[o];
   const uint64_t so = a.stake[org];
   uint32_t npr_sum = 0;
   uint32_t meta_next = tid < N ? ntl(&a.cmeta[base + tid]) : 0u;
@@ -903,7 +906,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
         continue;
       }
       const uint64_t sv = a.stake[v];
-      const uint32_t npr = prune_lane<ASZP>(a, mkw, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr));
+      const uint32_t npr = prune_lane<ASZP>(a, mkw, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, rwg_thr(a, o)));
       npr_sum += npr;
       finish_node(a, p, meta, len, 0, npr, true);
     } else {
@@ -932,7 +935,7 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
       uint32_t npr = 0;
       if (due) {
         const uint64_t sv = a.stake[v];
-        npr = prune_wave<ASZP>(a, mkw, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, thr), scr);
+        npr = prune_wave<ASZP>(a, mkw, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, rwg_thr(a, o)), scr);
         if (lane == 0) npr_sum += npr;
       }
       if (lane == 0) finish_node(a, p, meta, len, due ? 0u : up, npr, due);
