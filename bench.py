@@ -336,6 +336,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # GS_BENCH_DEVICE pins every rank to one device (rehearsing the multi-rank path on a one-GPU box)
+    dev = int(os.environ.get("GS_BENCH_DEVICE", local_rank))
     dist = None
     if world > 1:
         import torch
@@ -365,7 +367,7 @@ def main():
         origins, seed = all_origins, args.seed + rank
     S = len(origins)
     eng = gs.Engine(stakes, S, fanout=args.fanout, active_set_size=args.active_set_size,
-                    rotation_probability=args.rotation_probability, seed=seed, device=local_rank,
+                    rotation_probability=args.rotation_probability, seed=seed, device=dev,
                     bfs_mode=args.bfs_mode, profile=not args.no_profile, split_round=args.split_round)
     eng.set_slots(origins, args.min_ingress, args.threshold)
     eng.init_active_sets()
@@ -416,7 +418,7 @@ def main():
                                  row_bytes=summ.dtype.itemsize)
         if rank == 0 and args.check_shard:
             ref = gs.Engine(stakes, S_all, fanout=args.fanout, active_set_size=asz,
-                            rotation_probability=args.rotation_probability, seed=args.seed, device=local_rank,
+                            rotation_probability=args.rotation_probability, seed=args.seed, device=dev,
                             bfs_mode=args.bfs_mode)
             ref.set_slots(all_origins, args.min_ingress, args.threshold)
             ref.init_active_sets()
