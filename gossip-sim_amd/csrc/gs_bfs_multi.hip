@@ -82,7 +82,6 @@ struct MvArgs {
   uint32_t N, SP, ASZ, fanout, capin, s0, Sg, UB, BSC, BSF, nbc, nbf, TW, ORW, any_fail, gcap, gcap_c;
   uint32_t lane_c, wave_c, record;
   unsigned long long* pclk;  // GS_PHASE_PROFILE: gather phase clocks at [12..15] (thread 0 of each workgroup)
-  uint32_t exp;  // GS_MV_EXP (timing experiments only): 1 = gather writes no inbound rows (breaks results)
   uint32_t gh;  // gather: nodes with more records (all slots) take the wave path
   // nodes with per-pair state [vlo, vhi) (= fine bins [flo, flo + fno)); pair = slot * NP + node - vlo.
   // A node-range partition rank runs the whole BFS but keeps the records, counts and
@@ -786,7 +785,7 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             if (r + t >= r1 || !((m[t] >> j) & 1u)) continue;
-            if (cc < a.capin && !(a.exp & 1)) a.inb[(size_t)cc * a.PAIRS + p] = k[t];
+            if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = k[t];
             mh = min(mh, k[t] >> 24);
             ++cc;
           }
@@ -978,7 +977,8 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   g.UB = std::max(1u, ceil_log2(N));
   g.BSC = std::min(13u, std::max(6u, g.UB > 8 ? g.UB - 8 : 0u));   // ~256 coarse bins
   g.BSF = std::min(g.BSC, 9u);  // fine bins of <= 512 nodes (gather at C4: 301 vs 412 us with 1,024)
-  if (const char* x = std::getenv("GS_MV_BSF")) g.BSF = std::min(g.BSC, std::max(6u, (uint32_t)std::strtoul(x, nullptr, 10)));
+  // (GS_MV_BSF: tuning; at most 10 so that a partition range of whole 1,024-id bins is whole fine bins)
+  if (const char* x = std::getenv("GS_MV_BSF")) g.BSF = std::min(std::min(g.BSC, 10u), std::max(6u, (uint32_t)std::strtoul(x, nullptr, 10)));
   g.nbc = (N + (1u << g.BSC) - 1) >> g.BSC;
   g.nbf = g.nbc << (g.BSC - g.BSF);
   g.GW = std::min(28u, (64u - g.UB - g.BSC) & ~3u);
@@ -1085,8 +1085,6 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.gh = narrow ? 4u : 256u;  // C4: 291 us with no wave path, 311 at 32
   if (const char* x = std::getenv("GS_MV_GH")) a.gh = (uint32_t)std::strtoul(x, nullptr, 10);
   a.pclk = e.phase_clk;
-  a.exp = 0;
-  if (const char* x = std::getenv("GS_MV_EXP")) a.exp = (uint32_t)std::strtoul(x, nullptr, 10);
   a.record = 0;
   a.PAIRS = e.PAIRS; a.area_cap = e.mv.area_cap; a.rows_cap = e.mv.rows_cap; a.q_cap = e.mv.q_cap;
   a.pcap = e.mv.pcap;

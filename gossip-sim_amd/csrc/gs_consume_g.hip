@@ -55,7 +55,6 @@ struct CgArgs {
   uint32_t* prune_acc;
   uint32_t* err;
   uint32_t N, S, ASZ, capin, ORW;
-  uint32_t exp;  // GS_CG_EXP (timing experiments only, breaks results): 1 = prunes not applied to masks
   uint32_t NP, vlo;  // pair q = slot * NP + (node - vlo)
   size_t mso, msu;  // prune-mask strides of (slot, node)
   uint32_t lane_c, lane_l, wave_c;  // register-path bounds (16, 16) and wave-consume bound (64);
@@ -135,7 +134,7 @@ __device__ inline void apply_prune(const CgArgs& a, uint32_t o, uint32_t ob, uin
     const uint32_t pos = (uint32_t)s >= head ? (uint32_t)s - head : (uint32_t)s + a.ASZ - head;
     hit |= (uint32_t)((uint32_t)s < a.ASZ && pos < L && row[s] == v) << s;
   }
-  if (hit && !(a.exp & 1)) atomicOr(&a.mask[o * a.mso + u * a.msu], hit);
+  if (hit) atomicOr(&a.mask[o * a.mso + u * a.msu], hit);
 }
 
 // ---- prune, register path (len <= 32) ----
@@ -179,7 +178,7 @@ __device__ inline void prune_ranks(const CgArgs& a, uint32_t q, uint32_t o, uint
       if (k < CG_PL) {
         pl.u[k] = nd[i];
         pl.lane[k] = (uint8_t)lane_id();
-      } else if (!(a.exp & 2)) {
+      } else {
         apply_prune<ASZP>(a, o, ob, nd[i], v);
       }
     }
@@ -383,7 +382,7 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
       for (uint32_t k = lane_id(); k < pn; k += 64) {
         const uint32_t pq = qb + pl.lane[k];
         const uint32_t po = pq / a.NP;
-        if (!(a.exp & 2)) apply_prune<ASZP>(a, po, a.obkt[po], pl.u[k], a.vlo + (pq - po * a.NP));
+        apply_prune<ASZP>(a, po, a.obkt[po], pl.u[k], a.vlo + (pq - po * a.NP));
       }
       __builtin_amdgcn_wave_barrier();  // the list is reused by the wave's next pairs
     }
@@ -411,8 +410,6 @@ hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume) {
   CgArgs a;
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
   a.own = e.own; a.ORW = e.ORW;
-  a.exp = 0;
-  if (const char* x = std::getenv("GS_CG_EXP")) a.exp = (uint32_t)std::strtoul(x, nullptr, 10);
   a.min_ingress = e.min_ingress; a.thr = e.thr; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake; a.pinfo = e.pinfo;
   a.cnt = e.cnt; a.inb = e.inb; a.cmeta = e.cmeta; a.ckey = e.ckey; a.prune_round = e.prune_round;
   a.slot_prunes = e.slot_prunes; a.mask = e.mask; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc;
