@@ -500,8 +500,15 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
   }
   if (!in_lds) return;
   __syncthreads();  // of[i] is now the END of pair i's list
-  // 4. rows k of the bin, coalesced over pairs; per-pair state hoisted out of the k loop
+  // 4. rows k of the bin, coalesced over pairs; per-pair state hoisted out of the k loop.
+  // A wave loops to ITS largest count; pairs with more than G_HEAVY records are written
+  // afterwards by a whole wave each (lanes over k): power-law in-degrees (thousands at a
+  // 10M-node top-stake node) made every wave loop to the bin's largest count (kmax).
   constexpr uint32_t PPT = 4;  // BP / GATHER_THREADS pairs per thread (BP <= 2048 here; more loop below)
+  constexpr uint32_t G_HEAVY = 64;
+  (void)kmax;
+  uint32_t* hv = cb;  // the binned counts are dead once a step's c[] is loaded: the heavy list (i, n)
+  if (tid == 0) ctl[31] = 0;
   for (uint32_t i0 = 0; i0 < nq; i0 += PPT * GATHER_THREADS) {
     uint32_t c[PPT], st[PPT], sl[PPT];
 #pragma unroll
@@ -511,12 +518,39 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
       st[t] = i < nq ? of[i] - c[t] : 0u;
       sl[t] = i < nq ? cd[i] : 0u;
     }
-    for (uint32_t k = 0; k < kmax; ++k)
+    __syncthreads();  // every c[] of this step is loaded before the list overwrites cb
+    const uint32_t hcap = min(BP, i0 + PPT * GATHER_THREADS);  // counts of later steps stay intact
+    uint32_t cm = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < PPT; ++t) {
+      if (c[t] > G_HEAVY) {
+        const uint32_t h = atomicAdd(&ctl[31], 1u);
+        if (2 * h + 1 < hcap) {  // (a full list leaves the pair to the lane loop)
+          hv[2 * h] = i0 + t * GATHER_THREADS + tid;
+          hv[2 * h + 1] = c[t];
+          c[t] = 0;
+        }
+      }
+      cm = max(cm, c[t]);
+    }
+    for (int o = 32; o > 0; o >>= 1) cm = max(cm, (uint32_t)__shfl_xor((int)cm, o));
+    for (uint32_t k = 0; k < cm; ++k)
 #pragma unroll
       for (uint32_t t = 0; t < PPT; ++t) {
         const uint32_t i = i0 + t * GATHER_THREADS + tid;
         if (k < c[t] && sl[t] + k < a.capin) a.inb[(size_t)(sl[t] + k) * a.PAIRS + q0 + i] = csr[st[t] + k];
       }
+    __syncthreads();
+    const uint32_t nh = min(ctl[31], hcap / 2);
+    for (uint32_t h = tid >> 6; h < nh; h += GATHER_THREADS / 64) {
+      const uint32_t i = hv[2 * h], n = hv[2 * h + 1];
+      const uint32_t s0 = of[i] - n, d0 = cd[i];
+      for (uint32_t k = tid & 63; k < n; k += 64)
+        if (d0 + k < a.capin) a.inb[(size_t)(d0 + k) * a.PAIRS + q0 + i] = csr[s0 + k];
+    }
+    __syncthreads();
+    if (tid == 0) ctl[31] = 0;
+    __syncthreads();
   }
 }
 

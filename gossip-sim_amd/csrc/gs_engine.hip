@@ -355,6 +355,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   ALLOC(e->hist_acc, S * 256, 0);
   e->bm_words = (n + 31) / 32;
   ALLOC(e->bm, S * e->bm_words, 0);
+  ALLOC(e->bm_cnt, (size_t)S * 64, 0);
   // recorded-round summaries stay on the device until read back: a ring of up to
   // 256 MiB (C2: ~1,400 rounds) so a measured run is never stalled by a drain
   e->sum_cap = (uint32_t)std::max<size_t>(64, std::min<size_t>(4096, (256ull << 20) / (S * sizeof(gs_round_summary))));

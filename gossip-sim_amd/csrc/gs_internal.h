@@ -156,6 +156,7 @@ struct Engine {
   uint64_t* hist_acc = nullptr; // per slot: 256 hop bins over recorded rounds
   uint32_t* bm = nullptr;       // per slot: stranded bitmap over stake rank
   uint32_t bm_words = 0;
+  uint32_t* bm_cnt = nullptr;       // [S][64] set bits per 1/64 of each slot's stranded bitmap
   gs_round_summary* sum = nullptr;  // device ring of recorded summaries [sum_cap][S]
   uint32_t sum_cap = 0, sum_used = 0;
   std::vector<gs_round_summary> h_sum;  // drained summaries

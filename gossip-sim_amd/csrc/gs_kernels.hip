@@ -769,6 +769,7 @@ struct StatsArgs {
   uint32_t* rs_hist;
   uint64_t* hist_acc;
   uint32_t* bm;
+  uint32_t* bm_cnt;  // [S][64] set bits per chunk of each slot's bitmap (k_bm_count)
   gs_round_summary* sum;
   uint32_t N, S, W;
   uint32_t lo, hi;  // nodes of this pass (a node-range partition passes its own range)
@@ -863,6 +864,24 @@ __device__ void block_kth_bits(const uint32_t* __restrict__ bm, uint32_t W, cons
   __syncthreads();
 }
 
+// Set bits of each 1/64 of every slot's stranded bitmap (grid 64 x S): the finalize then
+// scans only the chunks holding its order statistics instead of one block walking the
+// whole bitmap twice (N / 32 words per slot: 312 K at 10M nodes).
+constexpr uint32_t BM_CHUNKS = 64;
+__global__ __launch_bounds__(256) void k_bm_count(const uint32_t* __restrict__ bm, uint32_t W, uint32_t* bm_cnt) {
+  const uint32_t o = blockIdx.y, b = blockIdx.x;
+  const uint32_t cw = (W + BM_CHUNKS - 1) / BM_CHUNKS;
+  const uint32_t lo = min(W, b * cw), hi = min(W, lo + cw);
+  const uint32_t* x = bm + (size_t)o * W;
+  uint32_t c = 0;
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) c += __popc(x[i]);
+  for (int off = 32; off > 0; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off);
+  __shared__ uint32_t ws[4];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bm_cnt[o * BM_CHUNKS + b] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
 __global__ __launch_bounds__(1024) void k_stats_finalize(StatsArgs a, uint32_t rec_slot) {
   const uint32_t o = blockIdx.x;
   __shared__ uint32_t hb[256];
@@ -940,7 +959,27 @@ __global__ __launch_bounds__(1024) void k_stats_finalize(StatsArgs a, uint32_t r
   if (sc) {
     const uint32_t klo = sc % 2 ? sc / 2 : sc / 2 - 1, khi = sc / 2;
     const uint32_t ks[4] = {0u, sc - 1, klo, khi};
-    block_kth_bits(bmo, a.W, ks, scratch, kth);
+    // the chunk of each order statistic (wave 0, one chunk per lane), then a block scan of
+    // that chunk only
+    __shared__ uint32_t kc[4], kr[4], ktmp[4];
+    if (threadIdx.x < 64) {
+      const uint32_t l = threadIdx.x;
+      const uint32_t c = a.bm_cnt[o * BM_CHUNKS + l];
+      const uint32_t incl = wave_incl_scan(c), before = incl - c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ks[j] >= before && ks[j] < incl) { kc[j] = l; kr[j] = ks[j] - before; }
+    }
+    __syncthreads();
+    const uint32_t cw = (a.W + BM_CHUNKS - 1) / BM_CHUNKS;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = min(a.W, kc[j] * cw), n = min(a.W, lo + cw) - lo;
+      const uint32_t kj[4] = {kr[j], 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      block_kth_bits(bmo + lo, n, kj, scratch, ktmp);  // (ends with a barrier)
+      if (threadIdx.x == 0) kth[j] = lo * 32 + ktmp[0];
+      __syncthreads();
+    }
     s.stranded_stake_min = a.stake[a.by_srank[kth[0]]];
     s.stranded_stake_max = a.stake[a.by_srank[kth[1]]];
     s.stranded_med_lo = a.stake[a.by_srank[kth[2]]];
@@ -967,7 +1006,7 @@ hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   a.hops = e.hops; a.cnt = e.cnt; a.egress = e.egress; a.prune_round = e.prune_round; a.slot_prunes = e.slot_prunes;
   a.egress_acc = e.egress_acc; a.ingress_acc = e.ingress_acc; a.prune_acc = e.prune_acc; a.strand = e.strand;
   a.rs_u32 = e.rs_u32; a.rs_ssum = e.rs_ssum; a.rs_hist = e.rs_hist; a.hist_acc = e.hist_acc; a.bm = e.bm;
-  a.sum = e.sum; a.N = e.N; a.S = e.S; a.W = e.bm_words; a.eso = e.eso; a.esu = e.esu;
+  a.sum = e.sum; a.N = e.N; a.S = e.S; a.W = e.bm_words; a.eso = e.eso; a.esu = e.esu; a.bm_cnt = e.bm_cnt;
   a.lo = e.vlo;
   a.hi = e.vlo + e.NP;
   a.NP = e.NP; a.vlo = e.vlo;
@@ -976,7 +1015,10 @@ hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   else if (mode == 1) hipLaunchKernelGGL(k_stats_pass<false>, dim3(gx, e.S), dim3(256), 0, e.st, a);
   else if (mode == 4 || mode == 5) hipLaunchKernelGGL((k_stats_pass<false, true>), dim3(gx, e.S), dim3(256), 0, e.st, a);
   if (mode != 3 && mode != 5)  // the pass only (a partition sums the partials over ranks first)
+  {
+    hipLaunchKernelGGL(k_bm_count, dim3(BM_CHUNKS, e.S), dim3(256), 0, e.st, e.bm, e.bm_words, e.bm_cnt);
     hipLaunchKernelGGL(k_stats_finalize, dim3(e.S), dim3(1024), 0, e.st, a, rec_slot);
+  }
   return hipGetLastError();
 }
 
