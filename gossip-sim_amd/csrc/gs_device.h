@@ -115,27 +115,26 @@ __device__ inline uint32_t prefix_search(const uint64_t* __restrict__ P, uint32_
   return lo;
 }
 
-// prefix_search with a coarse table PS[j] = P[min(j * PS_STRIDE, n)] (L2-resident): the
-// coarse search narrows the answer to one stride of P (2 KiB), the fine one finishes it.
-constexpr uint32_t PS_LOG = 5, PS_STRIDE = 1u << PS_LOG;
-__host__ __device__ inline uint32_t ps_count(uint32_t n) { return (n >> PS_LOG) + 2; }
-__device__ inline uint32_t prefix_search2(const uint64_t* __restrict__ P, const uint64_t* __restrict__ PS,
-                                          uint32_t n, uint64_t x) {
-  // smallest j in [1, m) with PS[j] > x (m: none)
-  const uint32_t m = ps_count(n);
-  uint32_t lo = 1, hi = m;
+// prefix_search through an index table: IX[j] = the answer for x_j = floor(total * j / 2^L)
+// (j <= 2^L), so the answer for x lies in [IX[j], IX[j + 1]] with j = floor(x * 2^L / total)
+// (answers are monotone in x and x_j <= x <= x_{j+1}): one table load, then a short
+// search of P instead of a search of the whole prefix array.
+__host__ __device__ inline uint32_t ix_log(uint32_t n) {
+  uint32_t l = 0;
+  while ((1u << l) < n) ++l;
+  l = l > 2 ? l - 2 : 0;
+  return l < 4 ? 4 : (l > 16 ? 16 : l);
+}
+__host__ __device__ inline uint32_t ix_count(uint32_t n) { return (1u << ix_log(n)) + 1; }
+__device__ inline uint32_t prefix_search_ix(const uint64_t* __restrict__ P, const uint32_t* __restrict__ IX,
+                                            uint32_t L, uint64_t total, uint64_t x) {
+  const uint32_t j = (uint32_t)((x << L) / total);  // x < total <= 625 * 2^24: no overflow
+  uint32_t lo = IX[j], hi = IX[j + 1];
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (PS[mid] > x) hi = mid; else lo = mid + 1;
+    if (P[mid + 1] > x) hi = mid; else lo = mid + 1;
   }
-  // answer i = smallest index in [flo, fhi] with P[i] > x; returns i - 1
-  uint32_t flo = (lo - 1) << PS_LOG, fhi = min(n, lo << PS_LOG);
-  flo = flo + 1 < fhi ? flo + 1 : fhi;
-  while (flo < fhi) {
-    const uint32_t mid = (flo + fhi) >> 1;
-    if (P[mid] > x) fhi = mid; else flo = mid + 1;
-  }
-  return flo - 1;
+  return lo;
 }
 
 // One WeightedShuffle step over the remaining candidates: given v uniform in
@@ -144,14 +143,15 @@ __device__ inline uint32_t prefix_search2(const uint64_t* __restrict__ P, const 
 // walking them in order shifts v past each excluded weight lying before the
 // answer, so a single search over the full prefix array finds it.
 template <int R>
-__device__ inline uint32_t shuffle_pick(const uint64_t* __restrict__ P, const uint64_t* __restrict__ PS, uint32_t n,
-                                        uint64_t v, const uint32_t (&rem)[R], const uint64_t (&remw)[R], int nr) {
+__device__ inline uint32_t shuffle_pick(const uint64_t* __restrict__ P, const uint32_t* __restrict__ IX, uint32_t L,
+                                        uint64_t total, uint64_t v, const uint32_t (&rem)[R],
+                                        const uint64_t (&remw)[R], int nr) {
   uint64_t x = v;
   for (int i = 0; i < nr; ++i) {
     if (P[rem[i]] <= x) x += remw[i];
     else break;
   }
-  return prefix_search2(P, PS, n, x);
+  return prefix_search_ix(P, IX, L, total, x);
 }
 
 template <int R>

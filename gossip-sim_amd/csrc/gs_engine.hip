@@ -265,7 +265,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   ALLOC(e->stake, N, 0);
   ALLOC(e->bucket, N, 0);
   ALLOC(e->P, (size_t)NB * (N + 1), 0);
-  ALLOC(e->PS, (size_t)NB * ps_count(n), 0);
+  ALLOC(e->IX, (size_t)NB * ix_count(n), 0);
   ALLOC(e->peers, N * NB * e->ASZP, 0);
   ALLOC(e->hl, N * NB, 0);
   ALLOC(e->frank, N, 0);

@@ -62,7 +62,7 @@ struct Engine {
   uint64_t* stake = nullptr;
   uint8_t* bucket = nullptr;
   uint64_t* P = nullptr;
-  uint64_t* PS = nullptr;        // [25][ps_count(N)] every 256th prefix sum (two-level weighted search)
+  uint32_t* IX = nullptr;        // [25][ix_count(N)] index tables of the prefix sums (prefix_search_ix)
   uint32_t* peers = nullptr;
   uint16_t* hl = nullptr;
   uint32_t* frank = nullptr;

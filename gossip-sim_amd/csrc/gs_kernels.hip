@@ -25,10 +25,9 @@ static inline uint32_t grid_for(size_t n, uint32_t block, uint32_t cap = 1u << 2
 
 // -------------------------------------------------------------- weights ----
 __global__ __launch_bounds__(1024) void k_prefix_weights(const uint8_t* __restrict__ bucket, uint64_t* __restrict__ P,
-                                                        uint64_t* __restrict__ PS, uint32_t N) {
+                                                        uint32_t N) {
   const int k = blockIdx.x;
   uint64_t* Pk = P + (size_t)k * (N + 1);
-  uint64_t* PSk = PS + (size_t)k * ps_count(N);
   const uint32_t T = blockDim.x, t = threadIdx.x;
   const uint32_t chunk = (N + T - 1) / T;
   const uint32_t lo = min(N, t * chunk), hi = min(N, lo + chunk);
@@ -44,19 +43,29 @@ __global__ __launch_bounds__(1024) void k_prefix_weights(const uint8_t* __restri
     __syncthreads();
   }
   uint64_t run = part[t] - s;
-  if (t == 0) { Pk[0] = 0; PSk[0] = 0; }
+  if (t == 0) Pk[0] = 0;
   for (uint32_t i = lo; i < hi; ++i) {
     run += weight(k, bucket[i]);
     Pk[i + 1] = run;
-    if (((i + 1) & (PS_STRIDE - 1)) == 0) PSk[(i + 1) >> PS_LOG] = run;
   }
-  if (t == T - 1) {  // samples past the end repeat the total: PS[j] = P[min(j * stride, N)]
-    for (uint32_t j = (N >> PS_LOG) + 1; j < ps_count(N); ++j) PSk[j] = run;
+}
+
+// The index table of each entry k's prefix sums (prefix_search_ix): IX[k][j] = the
+// smallest c with P[c + 1] > floor(total * j / 2^L), j = 0 .. 2^L.
+__global__ void k_build_ix(const uint64_t* __restrict__ P, uint32_t N, uint32_t* __restrict__ IX) {
+  const uint32_t L = ix_log(N), m = ix_count(N);
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < (uint32_t)NB * m; g += gridDim.x * blockDim.x) {
+    const uint32_t k = g / m, j = g - k * m;
+    const uint64_t* Pk = P + (size_t)k * (N + 1);
+    const uint64_t x = (Pk[N] * (uint64_t)j) >> L;
+    IX[g] = prefix_search(Pk, N, x);
   }
 }
 
 hipError_t launch_prefix_weights(Engine& e) {
-  hipLaunchKernelGGL(k_prefix_weights, dim3(NB), dim3(1024), 0, e.st, e.bucket, e.P, e.PS, e.N);
+  hipLaunchKernelGGL(k_prefix_weights, dim3(NB), dim3(1024), 0, e.st, e.bucket, e.P, e.N);
+  hipLaunchKernelGGL(k_build_ix, dim3(grid_for((size_t)NB * ix_count(e.N), 256, 4096)), dim3(256), 0, e.st, e.P, e.N,
+                     e.IX);
   return hipGetLastError();
 }
 
@@ -66,7 +75,7 @@ hipError_t launch_prefix_weights(Engine& e) {
 // 2..size+1 (or every candidate when N - 1 <= size).
 template <int ASZP>
 __global__ __launch_bounds__(256) void k_init_entries(const uint8_t* __restrict__ bucket,
-                                                     const uint64_t* __restrict__ P, const uint64_t* __restrict__ PS,
+                                                     const uint64_t* __restrict__ P, const uint32_t* __restrict__ IX,
                                                      uint32_t* __restrict__ peers,
                                                      uint16_t* __restrict__ hl, uint32_t N, uint32_t size,
                                                      uint64_t seed) {
@@ -74,14 +83,16 @@ __global__ __launch_bounds__(256) void k_init_entries(const uint8_t* __restrict_
   if (gid >= N * NB) return;
   const uint32_t u = gid / NB, k = gid % NB;
   const uint64_t* Pk = P + (size_t)k * (N + 1);
-  const uint64_t* PSk = PS + (size_t)k * ps_count(N);
+  const uint32_t L = ix_log(N);
+  const uint32_t* IXk = IX + (size_t)k * ix_count(N);
   constexpr int R = ASZP + 2;
   uint32_t rem[R];
   uint64_t remw[R];
   int nr = 0;
   const uint64_t wself = weight(k, bucket[u]);
   rem_insert(rem, remw, nr, u, wself);
-  uint64_t left = Pk[N] - wself;
+  const uint64_t total = Pk[N];
+  uint64_t left = total - wself;
   const uint32_t ncand = N - 1;
   const uint32_t T = min(ncand, size + 1);
   const bool drop = ncand >= size + 1;
@@ -90,7 +101,7 @@ __global__ __launch_bounds__(256) void k_init_entries(const uint8_t* __restrict_
   uint32_t filled = 0;
   for (uint32_t t = 0; t < T; ++t) {
     const uint64_t v = sample_below(left, s);
-    const uint32_t c = shuffle_pick(Pk, PSk, N, v, rem, remw, nr);
+    const uint32_t c = shuffle_pick(Pk, IXk, L, total, v, rem, remw, nr);
     const uint64_t wc = weight(k, bucket[c]);
     left -= wc;
     rem_insert(rem, remw, nr, c, wc);
@@ -102,7 +113,7 @@ __global__ __launch_bounds__(256) void k_init_entries(const uint8_t* __restrict_
 hipError_t launch_init_entries(Engine& e) {
   const uint32_t total = e.N * NB;
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_init_entries<A>, dim3(grid_for(total, 256)), dim3(256), 0, e.st,
-                                              e.bucket, e.P, e.PS, e.peers, e.hl, e.N, e.ASZ, e.prm.seed));
+                                              e.bucket, e.P, e.IX, e.peers, e.hl, e.N, e.ASZ, e.prm.seed));
   hipError_t r = hipGetLastError();
   return r != hipSuccess ? r : launch_own_rows(e, nullptr, nullptr);
 }
@@ -174,7 +185,7 @@ __global__ __launch_bounds__(1024) void k_rotate_decide(uint32_t N, uint64_t see
 // then drops the oldest: the ring's head slot is overwritten.
 template <int ASZP>
 __global__ __launch_bounds__(256) void k_rotate_entries(const uint8_t* __restrict__ bucket,
-                                                       const uint64_t* __restrict__ P, const uint64_t* __restrict__ PS,
+                                                       const uint64_t* __restrict__ P, const uint32_t* __restrict__ IX,
                                                        uint32_t* __restrict__ peers,
                                                        uint16_t* __restrict__ hl, const uint32_t* __restrict__ rot_list,
                                                        const uint32_t* __restrict__ rot_count,
@@ -190,19 +201,21 @@ __global__ __launch_bounds__(256) void k_rotate_entries(const uint8_t* __restric
     const uint32_t S = size;
     uint32_t* row = peers + (size_t)ent * ASZP;
     const uint64_t* Pk = P + (size_t)k * (N + 1);
-    const uint64_t* PSk = PS + (size_t)k * ps_count(N);
+    const uint32_t LX = ix_log(N);
+    const uint32_t* IXk = IX + (size_t)k * ix_count(N);
     constexpr int R = ASZP + 2;
     uint32_t rem[R];
     uint64_t remw[R];
     int nr = 0;
     const uint64_t wself = weight(k, bucket[u]);
     rem_insert(rem, remw, nr, u, wself);
-    uint64_t left = Pk[N] - wself;
+    const uint64_t total = Pk[N];
+    uint64_t left = total - wself;
     Philox s(seed, P_ROTATE, u, (round << 5) | k);
     uint32_t changed = 0;
     for (uint32_t drawn = 0; drawn + 1 < N; ++drawn) {
       const uint64_t v = sample_below(left, s);
-      const uint32_t c = shuffle_pick(Pk, PSk, N, v, rem, remw, nr);
+      const uint32_t c = shuffle_pick(Pk, IXk, LX, total, v, rem, remw, nr);
       const uint64_t wc = weight(k, bucket[c]);
       left -= wc;
       if (nr < R) rem_insert(rem, remw, nr, c, wc);
@@ -263,7 +276,7 @@ hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear) {
   hipLaunchKernelGGL(k_rotate_decide, dim3(grid_for(e.N, 4096, 256)), dim3(1024), 0, e.st, e.N, e.prm.seed, round,
                      e.prm.rotation_probability, e.rot_list, cnt, e.rot_count + (par ^ 1u));
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_rotate_entries<A>, dim3(grid_for((size_t)e.N * NB, 256, 2048)),
-                                              dim3(256), 0, e.st, e.bucket, e.P, e.PS, e.peers, e.hl, e.rot_list, cnt,
+                                              dim3(256), 0, e.st, e.bucket, e.P, e.IX, e.peers, e.hl, e.rot_list, cnt,
                                               e.rot_changed, e.N, e.ASZ, e.prm.seed, round));
   hipError_t ro = launch_own_rows(e, e.rot_list, cnt);
   if (ro != hipSuccess) return ro;
