@@ -33,7 +33,7 @@ namespace gs {
 
 constexpr uint32_t X_PPT = 4;          // frontier pairs per expand thread
 constexpr uint32_t APPLY_THREADS = 256;
-constexpr uint32_t GATHER_THREADS = 512;
+constexpr uint32_t GATHER_THREADS_S = 512, GATHER_THREADS_L = 1024;
 constexpr uint32_t SEG_CHUNK = 1024;   // expand workgroups' segments scanned per apply chunk
 
 struct BinArgs {
@@ -395,7 +395,9 @@ __host__ __device__ inline size_t bin_gather_lds_bytes(uint32_t BS, uint32_t csr
 // becomes the round's in-degree. Records are numbered f over the bin's level runs in
 // level order; a thread takes f = tid + j * GATHER_THREADS and keeps its first G_CACHE
 // records in registers for the placement pass.
-template <class R>
+// GATHER_THREADS: 512 (two workgroups per CU, bins of 2^11 pairs) or 1,024 (one per CU
+// with 160 KB of LDS for bins of 2^12+: twice the waves to hide the pool loads' latency).
+template <class R, uint32_t GATHER_THREADS>
 __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
   using RT = typename R::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -508,7 +510,7 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
   constexpr uint32_t G_HEAVY = 64;
   (void)kmax;
   uint32_t* hv = cb;  // the binned counts are dead once a step's c[] is loaded: the heavy list (i, n)
-  if (tid == 0) ctl[31] = 0;
+  if (tid == 0) ctl[40] = 0;
   for (uint32_t i0 = 0; i0 < nq; i0 += PPT * GATHER_THREADS) {
     uint32_t c[PPT], st[PPT], sl[PPT];
 #pragma unroll
@@ -524,7 +526,7 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
 #pragma unroll
     for (uint32_t t = 0; t < PPT; ++t) {
       if (c[t] > G_HEAVY) {
-        const uint32_t h = atomicAdd(&ctl[31], 1u);
+        const uint32_t h = atomicAdd(&ctl[40], 1u);
         if (2 * h + 1 < hcap) {  // (a full list leaves the pair to the lane loop)
           hv[2 * h] = i0 + t * GATHER_THREADS + tid;
           hv[2 * h + 1] = c[t];
@@ -541,7 +543,7 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
         if (k < c[t] && sl[t] + k < a.capin) a.inb[(size_t)(sl[t] + k) * a.PAIRS + q0 + i] = csr[st[t] + k];
       }
     __syncthreads();
-    const uint32_t nh = min(ctl[31], hcap / 2);
+    const uint32_t nh = min(ctl[40], hcap / 2);
     for (uint32_t h = tid >> 6; h < nh; h += GATHER_THREADS / 64) {
       const uint32_t i = hv[2 * h], n = hv[2 * h + 1];
       const uint32_t s0 = of[i] - n, d0 = cd[i];
@@ -549,7 +551,7 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
         if (d0 + k < a.capin) a.inb[(size_t)(d0 + k) * a.PAIRS + q0 + i] = csr[s0 + k];
     }
     __syncthreads();
-    if (tid == 0) ctl[31] = 0;
+    if (tid == 0) ctl[40] = 0;
     __syncthreads();
   }
 }
@@ -639,7 +641,9 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
   const uint32_t bgrid = ((a.nbins + 7) / 8) * 8;
   if ((r = hipFuncSetAttribute((const void*)k_bin_apply<R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a)))
     return r;
-  if ((r = hipFuncSetAttribute((const void*)k_bin_gather<R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
+  if ((r = hipFuncSetAttribute((const void*)k_bin_gather<R, GATHER_THREADS_S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
+    return r;
+  if ((r = hipFuncSetAttribute((const void*)k_bin_gather<R, GATHER_THREADS_L>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
     return r;
   GS_ASZP_DISPATCH(e.ASZP, {
     r = hipFuncSetAttribute((const void*)k_bin_expand<A, R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
@@ -656,7 +660,8 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
       if ((r = hipMemcpyAsync(h, e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st)) != hipSuccess) return r;
       if ((r = hipStreamSynchronize(e.st)) != hipSuccess) return r;
       if (*h == 0) {
-        hipLaunchKernelGGL(k_bin_gather<R>, dim3(bgrid), dim3(GATHER_THREADS), lds_g, e.st, a);
+        if (a.BS <= 11) hipLaunchKernelGGL((k_bin_gather<R, GATHER_THREADS_S>), dim3(bgrid), dim3(GATHER_THREADS_S), lds_g, e.st, a);
+        else hipLaunchKernelGGL((k_bin_gather<R, GATHER_THREADS_L>), dim3(bgrid), dim3(GATHER_THREADS_L), lds_g, e.st, a);
         return hipGetLastError();
       }
     }

@@ -416,6 +416,32 @@ def test_binned_bfs_matches_level_bfs_large(all_levels, wide):
             np.testing.assert_array_equal(x, y)
 
 
+def test_binned_bfs_large_bins_matches_level_bfs():
+    """More than 2^24 pairs (1.5M nodes x 12 slots): the binned BFS takes bins of 2^12 pairs,
+    8-byte records and the 1,024-thread gather with 160 KB of LDS. Equal to the level BFS
+    (hops, counters, summaries)."""
+    n, S = 1_500_000, 12
+    st = eb.synth.power_law_stakes(n)
+    origins = [int(x) for x in np.argsort(-st.astype(np.float64), kind="stable")[:S]]
+    engs = [gs.Engine(st, S, seed=41, rotation_probability=0.013333, bfs_mode=m)
+            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED)]
+    for e in engs:
+        e.set_slots(origins, 2, [0.05 * (1 + k % 6) for k in range(S)])
+        e.init_active_sets()
+        e.fail_nodes([0.0, 0.1] * (S // 2))
+    for r in range(3):
+        for e in engs:
+            e.round(r, record=True)
+    a, b = engs
+    np.testing.assert_array_equal(a.summaries(), b.summaries())
+    for k in (0, 5, 11):
+        np.testing.assert_array_equal(a.hops(k), b.hops(k))
+        for x, y in zip(a.counters(k), b.counters(k)):
+            np.testing.assert_array_equal(x, y)
+    for e in engs:
+        e.close()
+
+
 # ------------------------------------------- one-kernel workgroup round ----
 def run_fused_parity(n, S, rounds, *, fanout=6, asz=12, p=0.02, thr=0.15, mi=2, seed=11, check=(0, 1, 2, 3),
                      fail_at=None, fraction=0.0, full_every=5, narrow=False, origins=None, record_from=3):
