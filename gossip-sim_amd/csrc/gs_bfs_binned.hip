@@ -26,6 +26,7 @@
 //
 // Results equal k_bfs_level's: hops, in-degrees, the inbound record SET of each pair
 // (consume sorts them by (hop, src), gossip.rs:639-645), egress, frontier sizes.
+#include <type_traits>
 #include "gs_device.h"
 #include "gs_internal.h"
 
@@ -383,6 +384,115 @@ __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t
   }
 }
 
+// Wide records carry their global pair index, so one apply workgroup can take a SUPER-BIN
+// of 2^SB_LOG consecutive bins: the rows of T are read once per super-bin (one range
+// [T[w][b0], T[w][b0 + 16]) per expand workgroup) instead of once per bin -- with
+// thousands of bins (10M-node clusters) every bin's workgroup read a scattered word of
+// every T row, twice. Each record goes to its own bin's pool region (per-bin cursors in
+// LDS); first arrivals and the next frontier as in k_bin_apply.
+constexpr uint32_t SB_LOG = 2, SB_N = 1u << SB_LOG;  // C5: 4,017 us of BFS per round at 4 bins, 4,067 at 2, 4,548 at 8, 5,755 at 16; 4,811 per bin
+__host__ __device__ inline size_t bin_apply_sb_lds_bytes(uint32_t BS) {
+  return 4 * (2 * (size_t)SEG_CHUNK + 1 + 2 * SB_N * (((size_t)1 << BS) / 32) + 2 * SB_N + 64);
+}
+
+__global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply_sb(BinArgs a, uint32_t d, uint32_t* __restrict__ qnxt) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t qn = a.lvl[d];
+  if (qn == 0 || qn < a.qmin) return;  // (a direct level: no Lt entry, the gather skips it)
+  const uint32_t nb = a.nbins, nsb = (nb + SB_N - 1) >> SB_LOG;
+  const uint32_t B = xcd_bin(blockIdx.x, nsb);
+  if (B >= nsb) return;
+  const uint32_t tid = threadIdx.x, BS = a.BS, BP = 1u << BS, NW = BP / 32;
+  const uint32_t b0 = B << SB_LOG, nbb = min(SB_N, nb - b0), NWS = nbb * NW;
+  const uint32_t G = (qn + a.PW - 1) / a.PW;
+  uint32_t* pre = reinterpret_cast<uint32_t*>(smem);  // [SEG_CHUNK + 1]
+  uint32_t* sb = pre + SEG_CHUNK + 1;                 // [SEG_CHUNK]
+  uint32_t* vis = sb + SEG_CHUNK;                     // [SB_N * NW]
+  uint32_t* vis0 = vis + SB_N * NW;                   // [SB_N * NW]
+  uint32_t* cur = vis0 + SB_N * NW;                   // [SB_N] records appended per bin this level
+  uint32_t* bo = cur + SB_N;                          // [SB_N] the bins' pool fills before this level
+  uint32_t* ctl = bo + SB_N;                          // [64]: [1] frontier base, [8..] scan words
+  const size_t q0 = (size_t)b0 << BS;                 // the super-bin's first pair
+  for (uint32_t i = tid; i < NWS; i += APPLY_THREADS) {
+    const uint32_t m = a.visbm[(q0 >> 5) + i];
+    vis[i] = m;
+    vis0[i] = m;
+  }
+  if (tid < SB_N) {
+    cur[tid] = 0;
+    bo[tid] = tid < nbb ? a.binoff[b0 + tid] : 0u;
+  }
+  __syncthreads();
+  const uint32_t rec_hop = (d + 1) << 24;
+  const uint2* area = reinterpret_cast<const uint2*>(a.area);
+  uint2* pool = reinterpret_cast<uint2*>(a.pool);
+  for (uint32_t c0 = 0; c0 < G; c0 += SEG_CHUNK) {
+    const uint32_t gc = min(SEG_CHUNK, G - c0);
+    for (uint32_t i = tid; i < gc; i += APPLY_THREADS) {
+      const uint32_t* Tw = a.T + (size_t)(c0 + i) * (nb + 1);
+      const uint32_t st = Tw[b0];
+      pre[i] = Tw[b0 + nbb] - st;  // (Tw[nb] is the run's total: b0 + nbb <= nb)
+      sb[i] = st;
+    }
+    __syncthreads();
+    const uint32_t ct = block_excl_scan(pre, gc, ctl + 8);
+    if (tid == 0) pre[gc] = ct;
+    __syncthreads();
+    for (uint32_t r = tid; r < ct; r += APPLY_THREADS) {
+      uint32_t lo = 0, hi = gc;  // largest i with pre[i] <= r
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= r) lo = mid; else hi = mid;
+      }
+      const uint2 rec = area[(size_t)(c0 + lo) * a.PW * a.fc + sb[lo] + (r - pre[lo])];
+      uint32_t ql = (uint32_t)(rec.x - q0);  // pair within the super-bin
+      if (GS_OOB(ql, nbb * BP, a.err, "binned record pair")) ql = 0;
+      const uint32_t j = ql >> BS;
+      const uint32_t pos = atomicAdd(&cur[j], 1u);
+      if ((size_t)bo[j] + pos < a.pool_bin_cap)
+        pool[(size_t)(b0 + j) * a.pool_bin_cap + bo[j] + pos] = RecW::pool(ql & (BP - 1), rec_hop, rec.y);
+      atomicOr(&vis[ql >> 5], 1u << (ql & 31));
+    }
+    __syncthreads();
+  }
+  uint2* Ltd = a.Lt + (size_t)d * nb;
+  if (tid < nbb) {  // each bin's run of this level
+    const uint32_t used = bo[tid], n = cur[tid];
+    const bool over = (size_t)used + n > a.pool_bin_cap;
+    if (over) atomicOr(a.err, ERR_INBOUND);
+    Ltd[b0 + tid] = make_uint2((uint32_t)((size_t)(b0 + tid) * a.pool_bin_cap + used), over ? 0u : n);
+    if (!over) a.binoff[b0 + tid] = used + n;
+  }
+  // first arrivals (hop d + 1) and the next frontier in pair order: a contiguous run of
+  // bitmap words per thread
+  const uint32_t per = (NWS + APPLY_THREADS - 1) / APPLY_THREADS;
+  const uint32_t wlo = min(NWS, tid * per), whi = min(NWS, wlo + per);
+  uint32_t c = 0;
+  for (uint32_t w = wlo; w < whi; ++w) c += __popc(vis[w] & ~vis0[w]);
+  const uint32_t incl = wave_incl_scan(c);
+  if ((tid & 63) == 63) ctl[8 + (tid >> 6)] = incl;
+  __syncthreads();
+  uint32_t off = 0, tnew = 0;
+  for (uint32_t k = 0; k < APPLY_THREADS / 64; ++k) {
+    if (k < (tid >> 6)) off += ctl[8 + k];
+    tnew += ctl[8 + k];
+  }
+  if (tnew == 0) return;
+  if (tid == 0) ctl[1] = atomicAdd(&a.lvl[d + 1], tnew);
+  __syncthreads();
+  uint32_t pos = ctl[1] + off + incl - c;
+  for (uint32_t w = wlo; w < whi; ++w) {
+    const uint32_t m = vis[w] & ~vis0[w];
+    if (!m) continue;
+    a.visbm[(q0 >> 5) + w] = vis[w];
+    for (uint32_t mm = m; mm; mm &= mm - 1) {
+      const uint32_t q = (uint32_t)(q0 + w * 32 + __ffs(mm) - 1);
+      qnxt[pos++] = q;
+      a.hops[q] = (uint8_t)(d + 1);
+    }
+  }
+}
+
 // gather LDS: direct-level in-degrees [BP], binned counts [BP], CSR cursors [BP], CSR [csr_cap],
 // per-level run table [3][256] + prefix [257], scan words
 constexpr uint32_t G_CACHE = 24;  // pool records per thread kept in registers between the passes
@@ -641,6 +751,12 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
   const uint32_t bgrid = ((a.nbins + 7) / 8) * 8;
   if ((r = hipFuncSetAttribute((const void*)k_bin_apply<R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a)))
     return r;
+  // wide records: super-bin apply (one workgroup per 16 bins)
+  constexpr bool SBA = std::is_same<R, RecW>::value;
+  const size_t lds_sb = bin_apply_sb_lds_bytes(a.BS);
+  const uint32_t sbgrid = ((((a.nbins + SB_N - 1) >> SB_LOG) + 7) / 8) * 8;
+  if (SBA && (r = hipFuncSetAttribute((const void*)k_bin_apply_sb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sb)))
+    return r;
   if ((r = hipFuncSetAttribute((const void*)k_bin_gather<R, GATHER_THREADS_S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
     return r;
   if ((r = hipFuncSetAttribute((const void*)k_bin_gather<R, GATHER_THREADS_L>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
@@ -652,7 +768,8 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
   for (uint32_t d = 0; d < 254; ++d) {
     GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_expand<A, R>), dim3(xgrid), dim3(xth), lds_x, e.st, a, d,
                                                 e.q[d & 1], e.q[(d + 1) & 1]));
-    hipLaunchKernelGGL(k_bin_apply<R>, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
+    if (SBA) hipLaunchKernelGGL(k_bin_apply_sb, dim3(sbgrid), dim3(APPLY_THREADS), lds_sb, e.st, a, d, e.q[(d + 1) & 1]);
+    else hipLaunchKernelGGL(k_bin_apply<R>, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
     // poll the frontier size after 12 levels, then every 4: a poll idles the GPU for a
     // host round trip (~35 us), an empty level costs two no-op dispatches (~7 us)
     if (d >= 11 && (d & 3) == 3) {

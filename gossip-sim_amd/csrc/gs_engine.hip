@@ -308,7 +308,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     ALLOC(e->bin_pool, ((size_t)e->bin.nbins << e->bin.BS) * e->capin / (e->bin.narrow ? 2 : 1), 0);
     ALLOC(e->bin_Lt, (size_t)256 * e->bin.nbins, 0);
     ALLOC(e->bin_binoff, e->bin.nbins, 0);
-    ALLOC(e->bin_vis, (PAIRS + 31) / 32, 0);
+    ALLOC(e->bin_vis, (size_t)e->bin.nbins << (e->bin.BS - 5), 0);  // whole bins (applies read a bin's words)
   }
   if (mode == GS_BFS_MULTI) {
     const MvGeom& g = e->mv;
