@@ -122,13 +122,13 @@ __device__ inline uint32_t prefix_search(const uint64_t* __restrict__ P, uint32_
 __host__ __device__ inline uint32_t ix_log(uint32_t n) {
   uint32_t l = 0;
   while ((1u << l) < n) ++l;
-  l = l > 2 ? l - 2 : 0;
-  return l < 4 ? 4 : (l > 16 ? 16 : l);
+  l = l > 3 ? l - 3 : 0;  // ~8 candidates per table entry: ~3 steps of the search in P
+  return l < 4 ? 4 : (l > 20 ? 20 : l);
 }
 __host__ __device__ inline uint32_t ix_count(uint32_t n) { return (1u << ix_log(n)) + 1; }
 __device__ inline uint32_t prefix_search_ix(const uint64_t* __restrict__ P, const uint32_t* __restrict__ IX,
                                             uint32_t L, uint64_t total, uint64_t x) {
-  const uint32_t j = (uint32_t)((x << L) / total);  // x < total <= 625 * 2^24: no overflow
+  const uint32_t j = (uint32_t)((x << L) / total);  // x < total <= 625 * 2^24, L <= 20: no overflow
   uint32_t lo = IX[j], hi = IX[j + 1];
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
