@@ -60,6 +60,7 @@ struct BinArgs {
   uint2* Lt;       // [256][nbins] (pool start, count) of bin b's run at level d
   uint32_t* binoff;  // [nbins] records in bin b's pool region so far this round (only bin b's apply touches it)
   uint32_t* visbm;  // [PAIRS / 32] visited pairs (hop != unreached) of this round
+  uint32_t* hlvl;   // host-mapped [256]: expand(d) writes level d's frontier size
   uint32_t N, ASZ, fanout, fc, capin, Gmax, PW, BS, nbins, ORW, csr_cap, qmin;
   size_t PAIRS, pool_bin_cap;  // pool region of a bin: 2^BS * capin records (in-degrees are <= capin)
   int record;
@@ -208,12 +209,43 @@ __device__ inline void bin_direct(const BinArgs& a, uint32_t d, uint32_t qn, con
 
 // A level with fewer than qmin frontier pairs runs bin_direct in this same launch
 // (no dispatch of its own); a larger one is expanded into bin runs for k_bin_apply.
+// Direct levels of at most BIN_SMALL frontier pairs run inside ONE workgroup, level after
+// level, with no launch between them (bin_direct's device-scope atomics order the
+// level's first arrivals; the next level's size is read after a barrier). Starts at
+// level d0; stops at the first level with no pairs, more than BIN_SMALL, or at qmin;
+// writes (level, pairs) to the host-mapped hstate.
+constexpr uint32_t BIN_SMALL = 1024, BIN_ST = 1024;
+template <int ASZP>
+__global__ __launch_bounds__(BIN_ST) void k_bin_small(BinArgs a, uint32_t d0, uint32_t lim, uint32_t* __restrict__ q0,
+                                                     uint32_t* __restrict__ q1, uint32_t* __restrict__ hstate) {
+  __shared__ uint32_t s_qn;
+  uint32_t d = d0;
+  if (threadIdx.x == 0) s_qn = a.lvl[d0];
+  __syncthreads();
+  uint32_t qn = s_qn;
+  while (qn > 0 && qn <= lim && d < 254) {
+    if (threadIdx.x == 0) __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    bin_direct<ASZP>(a, d, qn, (d & 1) ? q1 : q0, (d & 1) ? q0 : q1);
+    __syncthreads();
+    if (threadIdx.x == 0) s_qn = __hip_atomic_load(&a.lvl[d + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    qn = s_qn;
+    ++d;
+  }
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&hstate[1], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hstate[0], d, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // the host polls this word
+  }
+}
+
 template <int ASZP, class R>
 __global__ __launch_bounds__(512) void k_bin_expand(BinArgs a, uint32_t d, const uint32_t* __restrict__ qcur,
                                                     uint32_t* __restrict__ qnxt) {
   using RT = typename R::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t qn = a.lvl[d];
+  if (blockIdx.x == 0 && threadIdx.x == 0)  // the host's level poll (host-mapped)
+    __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (qn < a.qmin) {
     bin_direct<ASZP>(a, d, qn, qcur, qnxt);
     return;
@@ -765,25 +797,43 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
     r = hipFuncSetAttribute((const void*)k_bin_expand<A, R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
   });
   if (r != hipSuccess) return r;
-  for (uint32_t d = 0; d < 254; ++d) {
-    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_expand<A, R>), dim3(xgrid), dim3(xth), lds_x, e.st, a, d,
-                                                e.q[d & 1], e.q[(d + 1) & 1]));
-    if (SBA) hipLaunchKernelGGL(k_bin_apply_sb, dim3(sbgrid), dim3(APPLY_THREADS), lds_sb, e.st, a, d, e.q[(d + 1) & 1]);
-    else hipLaunchKernelGGL(k_bin_apply<R>, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
-    // poll the frontier size after 12 levels, then every 4: a poll idles the GPU for a
-    // host round trip (~35 us), an empty level costs two no-op dispatches (~7 us)
-    if (d >= 11 && (d & 3) == 3) {
-      uint32_t* h = e.h_err + 1;
-      if ((r = hipMemcpyAsync(h, e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st)) != hipSuccess) return r;
-      if ((r = hipStreamSynchronize(e.st)) != hipSuccess) return r;
-      if (*h == 0) {
-        if (a.BS <= 11) hipLaunchKernelGGL((k_bin_gather<R, GATHER_THREADS_S>), dim3(bgrid), dim3(GATHER_THREADS_S), lds_g, e.st, a);
-        else hipLaunchKernelGGL((k_bin_gather<R, GATHER_THREADS_L>), dim3(bgrid), dim3(GATHER_THREADS_L), lds_g, e.st, a);
-        return hipGetLastError();
+  // Levels of at most `lim` frontier pairs run in one workgroup (k_bin_small); larger ones
+  // as expand + apply, the host enqueueing level d after seeing level d - lag's size
+  // (host-mapped, written by expand) so the GPU never idles for the host's reaction.
+  volatile uint32_t* hl = e.mv_hlvl;
+  volatile uint32_t* hs = e.mv_hlvl + 256;
+  uint32_t small = BIN_SMALL;
+  if (const char* x = std::getenv("GS_BIN_SMALL")) small = (uint32_t)std::strtoul(x, nullptr, 10);
+  const uint32_t lim = std::min(small, a.qmin - 1), lag = 2;
+  uint32_t d = 0;
+  for (;;) {
+    hs[0] = MV_PENDING;
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_small<A>), dim3(1), dim3(BIN_ST), 0, e.st, a, d, lim, e.q[0], e.q[1],
+                                                e.mv_hstate_dev));
+    if ((r = mv_wait(hs, e.st, d))) return r;
+    if (hs[1] == 0) break;
+    const uint32_t dl = d;
+    bool done = false;
+    for (;; ++d) {
+      if (d >= 254) return hipErrorNotSupported;  // frontier still non-empty: hop counts no longer fit u8
+      hl[d] = MV_PENDING;
+      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_expand<A, R>), dim3(xgrid), dim3(xth), lds_x, e.st, a, d,
+                                                  e.q[d & 1], e.q[(d + 1) & 1]));
+      if (SBA) hipLaunchKernelGGL(k_bin_apply_sb, dim3(sbgrid), dim3(APPLY_THREADS), lds_sb, e.st, a, d, e.q[(d + 1) & 1]);
+      else hipLaunchKernelGGL(k_bin_apply<R>, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
+      if (d >= dl + lag) {
+        uint32_t x = 0;
+        if ((r = mv_wait(hl + (d - lag), e.st, x))) return r;
+        if (x == 0) { done = true; break; }
+        if (x <= lim) { ++d; break; }  // levels through d are enqueued; small levels from d + 1
       }
     }
+    if (done) break;
+    if (d >= 254) return hipErrorNotSupported;
   }
-  return hipErrorNotSupported;  // frontier still non-empty after 254 levels: hop counts no longer fit u8
+  if (a.BS <= 11) hipLaunchKernelGGL((k_bin_gather<R, GATHER_THREADS_S>), dim3(bgrid), dim3(GATHER_THREADS_S), lds_g, e.st, a);
+  else hipLaunchKernelGGL((k_bin_gather<R, GATHER_THREADS_L>), dim3(bgrid), dim3(GATHER_THREADS_L), lds_g, e.st, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_bfs_binned(Engine& e, bool record) {
@@ -792,7 +842,7 @@ hipError_t launch_bfs_binned(Engine& e, bool record) {
   a.obkt = e.obkt; a.nfail = e.nfail; a.mask = e.mask; a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb;
   a.egress = e.egress; a.egress_acc = e.egress_acc; a.lvl = e.lvl; a.err = e.err; a.area = e.bin_area;
   a.T = e.bin_T; a.pool = e.bin_pool; a.Lt = e.bin_Lt; a.binoff = e.bin_binoff;
-  a.visbm = e.bin_vis;
+  a.visbm = e.bin_vis; a.hlvl = e.mv_hlvl_dev;
   a.N = e.N; a.ASZ = e.ASZ; a.fanout = e.fanout; a.fc = e.fcap; a.capin = e.capin; a.Gmax = e.bin.Gmax;
   a.PW = e.bin.PW; a.BS = e.bin.BS; a.nbins = e.bin.nbins; a.ORW = e.ORW; a.csr_cap = e.bin.csr_cap;
   a.qmin = (e.prm.flags & GS_FLAG_BINNED_ALL_LEVELS) ? 1u : BIN_MIN_FRONTIER;

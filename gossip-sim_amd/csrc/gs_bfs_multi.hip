@@ -1094,8 +1094,7 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
 // Host-mapped words the level loop polls: PENDING until the kernel that writes them
 // runs. The spin checks the stream now and then, so a stream that finished (or failed)
 // without writing the word ends the wait instead of hanging it.
-constexpr uint32_t MV_PENDING = 0xFFFFFFFFu;
-static hipError_t mv_wait(volatile uint32_t* p, hipStream_t st, uint32_t& out) {
+hipError_t mv_wait(volatile uint32_t* p, hipStream_t st, uint32_t& out) {
   for (uint64_t it = 1;; ++it) {
     const uint32_t x = *p;
     if (x != MV_PENDING) { out = x; return hipSuccess; }

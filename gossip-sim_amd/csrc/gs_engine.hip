@@ -310,6 +310,14 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     ALLOC(e->bin_binoff, e->bin.nbins, 0);
     ALLOC(e->bin_vis, (size_t)e->bin.nbins << (e->bin.BS - 5), 0);  // whole bins (applies read a bin's words)
   }
+  if (mode == GS_BFS_BINNED || mode == GS_BFS_MULTI) {  // host-mapped level sizes the level loops poll
+    if (hipHostMalloc(&e->mv_hlvl, 272 * 4, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&e->mv_hlvl_dev, e->mv_hlvl, 0) != hipSuccess) {
+      destroy_engine(e);
+      return fail(GS_ENOMEM, "host-mapped frontier counters");
+    }
+    e->mv_hstate_dev = e->mv_hlvl_dev + 256;
+  }
   if (mode == GS_BFS_MULTI) {
     const MvGeom& g = e->mv;
     if (const char* dg = std::getenv("GS_MV_DIAG"); dg && dg[0] == '1') e->mv_diag = true;
@@ -335,12 +343,6 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     ALLOC(e->mv_fcls, N, 0xFF);
     ALLOC(e->mv_fk, S, 0);
     ALLOC(e->mv_thr, S, 0);
-    if (hipHostMalloc(&e->mv_hlvl, 272 * 4, hipHostMallocMapped) != hipSuccess ||
-        hipHostGetDevicePointer((void**)&e->mv_hlvl_dev, e->mv_hlvl, 0) != hipSuccess) {
-      destroy_engine(e);
-      return fail(GS_ENOMEM, "host-mapped frontier counters");
-    }
-    e->mv_hstate_dev = e->mv_hlvl_dev + 256;
     ALLOC(e->mv_gtab, (size_t)((S + g.GW - 1) / g.GW) * GT_WORDS, 0);
     ALLOC(e->mv_seed, S, 0);
   }

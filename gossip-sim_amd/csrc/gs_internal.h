@@ -197,6 +197,10 @@ hipError_t launch_scatter_rank(Engine& e, const uint32_t* sorted_ids, uint32_t* 
 hipError_t launch_clear_slot_masks(Engine& e, uint32_t node, uint32_t bucket, uint32_t bits);
 hipError_t launch_bfs(Engine& e, bool record);
 hipError_t launch_bfs_binned(Engine& e, bool record);
+// spin on a host-mapped word the device writes (MV_PENDING until then); checks the stream
+// now and then so a stream that ended without writing it fails instead of hanging
+constexpr uint32_t MV_PENDING = 0xFFFFFFFFu;
+hipError_t mv_wait(volatile uint32_t* p, hipStream_t st, uint32_t& out);
 hipError_t launch_bfs_level_step(Engine& e, bool record, uint32_t d, uint32_t qmin, uint32_t qmax);
 void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g, bool allow_narrow);
 bool bin_supported(const BinGeom& g, uint32_t fcap);
