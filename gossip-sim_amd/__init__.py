@@ -27,6 +27,7 @@ GS_FLAG_SPLIT_ROUND = 2
 GS_FLAG_NARROW_WAVE_PATH = 4
 GS_FLAG_BINNED_ALL_LEVELS = 8
 GS_FLAG_WIDE_RECORDS = 16
+GS_FLAG_NO_SMALL_LEVELS = 32
 HOP_UNREACHED = 0xFF
 B58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
 
@@ -80,6 +81,9 @@ EXPORTS = {
     "gs_part_round": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.POINTER(C.c_uint32)]),
     "gs_part_prunes_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_part_prunes_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),
+    "gs_part_exchange_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "gs_part_prunes_dense_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "gs_part_prunes_dense_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_part_stats_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_part_stats_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_create": (C.c_int, [C.POINTER(Params), C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p)]),
@@ -185,7 +189,8 @@ class Engine:
 
     def __init__(self, stakes, n_slots, *, fanout=6, active_set_size=12, rotation_probability=0.013333, seed=0,
                  device=0, bfs_mode=GS_BFS_AUTO, inbound_capacity=0, profile=False, split_round=False,
-                 narrow_wave_path=False, binned_all_levels=False, wide_records=False, part=None):
+                 narrow_wave_path=False, binned_all_levels=False, wide_records=False, no_small_levels=False,
+                 part=None):
         L = lib()
         self.stakes = np.ascontiguousarray(stakes, dtype=np.uint64)
         self.n = len(self.stakes)
@@ -195,7 +200,7 @@ class Engine:
                    (GS_FLAG_PROFILE if profile else 0) | (GS_FLAG_SPLIT_ROUND if split_round else 0) |
                    (GS_FLAG_NARROW_WAVE_PATH if narrow_wave_path else 0) |
                    (GS_FLAG_BINNED_ALL_LEVELS if binned_all_levels else 0) |
-                   (GS_FLAG_WIDE_RECORDS if wide_records else 0))
+                   (GS_FLAG_WIDE_RECORDS if wide_records else 0) | (GS_FLAG_NO_SMALL_LEVELS if no_small_levels else 0))
         h = C.c_void_p()
         if part is None:
             _check(L.gs_create(C.byref(p), _ptr(self.stakes), self.n, n_slots, C.byref(h)))

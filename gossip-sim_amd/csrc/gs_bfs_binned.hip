@@ -350,16 +350,16 @@ __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t
     return;
   }
   // 2. the level's pool run for this bin
-  if (tid == 0) {  // the bin's own pool region: no device-wide counter
+  if (tid == 0) {  // the bin's own pool region: no device-wide counter; Lt holds the bin-relative start
     const uint32_t used = a.binoff[b];
-    const size_t base = (size_t)b * a.pool_bin_cap + used;
-    ctl[0] = (uint32_t)base;
+    ctl[0] = used;
     ctl[2] = 0;
     if ((size_t)used + total > a.pool_bin_cap) { atomicOr(a.err, ERR_INBOUND); ctl[2] = 1; }
     else a.binoff[b] = used + total;
-    Ltd[b] = make_uint2((uint32_t)base, ctl[2] ? 0u : total);
+    Ltd[b] = make_uint2(used, ctl[2] ? 0u : total);
   }
   __syncthreads();
+  RT* const bpool = reinterpret_cast<RT*>(a.pool) + (size_t)b * a.pool_bin_cap;  // (64-bit: the pool passes 2^32 records)
   const uint32_t pbase = ctl[0];
   const bool pool_ok = ctl[2] == 0;
   // 3. the records, one thread each, in chunks of SEG_CHUNK expand workgroups
@@ -386,7 +386,7 @@ __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t
       const RT rec = reinterpret_cast<const RT*>(a.area)[(size_t)(c0 + lo) * a.PW * a.fc + sb[lo] + (r - pre[lo])];
       uint32_t ql = R::area_ql(rec, q0);
       if (GS_OOB(ql, BP, a.err, "binned record pair")) ql = 0;
-      if (pool_ok) reinterpret_cast<RT*>(a.pool)[pbase + done + r] = R::pool(ql, rec_hop, R::area_src(rec));
+      if (pool_ok) bpool[pbase + done + r] = R::pool(ql, rec_hop, R::area_src(rec));
       atomicOr(&vis[ql >> 5], 1u << (ql & 31));
     }
     done += ct;
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply_sb(BinArgs a, uint3
     const uint32_t used = bo[tid], n = cur[tid];
     const bool over = (size_t)used + n > a.pool_bin_cap;
     if (over) atomicOr(a.err, ERR_INBOUND);
-    Ltd[b0 + tid] = make_uint2((uint32_t)((size_t)(b0 + tid) * a.pool_bin_cap + used), over ? 0u : n);
+    Ltd[b0 + tid] = make_uint2(used, over ? 0u : n);  // bin-relative start (the gather adds the bin's base)
     if (!over) a.binoff[b0 + tid] = used + n;
   }
   // first arrivals (hop d + 1) and the next frontier in pair order: a contiguous run of
@@ -543,9 +543,9 @@ template <class R, uint32_t GATHER_THREADS>
 __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
   using RT = typename R::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const RT* pool = reinterpret_cast<const RT*>(a.pool);
   const uint32_t b = xcd_bin(blockIdx.x, a.nbins);
   if (b >= a.nbins) return;
+  const RT* pool = reinterpret_cast<const RT*>(a.pool) + (size_t)b * a.pool_bin_cap;  // this bin's region; Lt is relative
   const uint32_t tid = threadIdx.x, nb = a.nbins, BP = 1u << a.BS;
   uint32_t* cd = reinterpret_cast<uint32_t*>(smem);  // [BP] direct-level in-degree
   uint32_t* cb = cd + BP;                            // [BP] binned-level records
@@ -804,18 +804,26 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
   volatile uint32_t* hs = e.mv_hlvl + 256;
   uint32_t small = BIN_SMALL;
   if (const char* x = std::getenv("GS_BIN_SMALL")) small = (uint32_t)std::strtoul(x, nullptr, 10);
+  if (e.prm.flags & GS_FLAG_NO_SMALL_LEVELS) small = 0;
   const uint32_t lim = std::min(small, a.qmin - 1), lag = 2;
   uint32_t d = 0;
   for (;;) {
     hs[0] = MV_PENDING;
     GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_small<A>), dim3(1), dim3(BIN_ST), 0, e.st, a, d, lim, e.q[0], e.q[1],
                                                 e.mv_hstate_dev));
+    e.bfs_level = d;
     if ((r = mv_wait(hs, e.st, d))) return r;
     if (hs[1] == 0) break;
     const uint32_t dl = d;
     bool done = false;
     for (;; ++d) {
-      if (d >= 254) return hipErrorNotSupported;  // frontier still non-empty: hop counts no longer fit u8
+      if (d >= 254) {  // levels through 253 enqueued: the hops fit u8 iff level 254 is empty
+        bool empty = false;
+        if ((r = level_empty(e, 254, empty))) return r;
+        if (!empty) return hipErrorNotSupported;
+        done = true;
+        break;
+      }
       hl[d] = MV_PENDING;
       GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_expand<A, R>), dim3(xgrid), dim3(xth), lds_x, e.st, a, d,
                                                   e.q[d & 1], e.q[(d + 1) & 1]));
@@ -823,13 +831,13 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
       else hipLaunchKernelGGL(k_bin_apply<R>, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
       if (d >= dl + lag) {
         uint32_t x = 0;
+        e.bfs_level = d - lag;
         if ((r = mv_wait(hl + (d - lag), e.st, x))) return r;
         if (x == 0) { done = true; break; }
         if (x <= lim) { ++d; break; }  // levels through d are enqueued; small levels from d + 1
       }
     }
     if (done) break;
-    if (d >= 254) return hipErrorNotSupported;
   }
   if (a.BS <= 11) hipLaunchKernelGGL((k_bin_gather<R, GATHER_THREADS_S>), dim3(bgrid), dim3(GATHER_THREADS_S), lds_g, e.st, a);
   else hipLaunchKernelGGL((k_bin_gather<R, GATHER_THREADS_L>), dim3(bgrid), dim3(GATHER_THREADS_L), lds_g, e.st, a);

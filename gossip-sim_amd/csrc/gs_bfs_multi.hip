@@ -33,6 +33,7 @@
 // to host-mapped memory and the host polls it two levels late (after an event).
 // Results equal k_bfs_level's: hops, in-degrees, inbound record sets, egress.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 
@@ -1072,6 +1073,7 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.vlo = e.vlo; a.vhi = e.vlo + e.NP; a.NP = e.NP; a.MSU = (uint32_t)e.msu;
   a.small = MV_SMALL;
   if (const char* sm = std::getenv("GS_MV_SMALL")) a.small = (uint32_t)std::strtoul(sm, nullptr, 10);
+  if (e.prm.flags & GS_FLAG_NO_SMALL_LEVELS) a.small = 0;  // every level through expand + apply
   a.flo = e.vlo >> e.mv.BSF; a.fno = mv_kept_bins(e);
   a.ORW = e.ORW;
   a.any_fail = 0;
@@ -1094,7 +1096,16 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
 // Host-mapped words the level loop polls: PENDING until the kernel that writes them
 // runs. The spin checks the stream now and then, so a stream that finished (or failed)
 // without writing the word ends the wait instead of hanging it.
+// The wait is bounded in wall-clock time (GS_LEVEL_WAIT_S, default 60 s): a kernel that
+// never finishes its level (a device-side livelock) ends in hipErrorLaunchTimeOut, which the
+// engine reports with the level, instead of spinning forever.
 hipError_t mv_wait(volatile uint32_t* p, hipStream_t st, uint32_t& out) {
+  static const double limit_s = [] {
+    const char* x = std::getenv("GS_LEVEL_WAIT_S");
+    const double v = x ? std::strtod(x, nullptr) : 0.0;
+    return v > 0 ? v : 60.0;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t it = 1;; ++it) {
     const uint32_t x = *p;
     if (x != MV_PENDING) { out = x; return hipSuccess; }
@@ -1105,8 +1116,18 @@ hipError_t mv_wait(volatile uint32_t* p, hipStream_t st, uint32_t& out) {
         return out != MV_PENDING ? hipSuccess : hipErrorUnknown;
       }
       if (q != hipErrorNotReady) return q;
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
+        return hipErrorLaunchTimeOut;
     }
   }
+}
+
+hipError_t level_empty(Engine& e, uint32_t d, bool& empty) {
+  uint32_t x = 0;
+  hipError_t r = hipMemcpyAsync(&x, e.lvl + d, 4, hipMemcpyDeviceToHost, e.st);
+  if (r == hipSuccess) r = hipStreamSynchronize(e.st);
+  empty = x == 0;
+  return r;
 }
 
 hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
@@ -1161,21 +1182,30 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       hs[0] = MV_PENDING;
       GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, d,
                                                   e.mv_q[0], e.mv_q[1], e.mv_hstate_dev));
-      if ((r = mv_wait(hs, e.st, d))) return r;
+      e.bfs_level = d;
+    if ((r = mv_wait(hs, e.st, d))) return r;
       if (hs[1] == 0) { nlev = d; break; }
       if (d >= 254) return hipErrorNotSupported;  // frontier still non-empty after 254 levels
       // large levels: expand + apply; the frontier size of level x is polled two levels late
       const uint32_t dl = d;
       bool done = false;
       for (;; ++d) {
-        if (d >= 254) return hipErrorNotSupported;
+        if (d >= 254) {  // levels through 253 enqueued: the hops fit u8 iff level 254 is empty
+          bool empty = false;
+          if ((r = level_empty(e, 254, empty))) return r;
+          if (!empty) return hipErrorNotSupported;
+          nlev = d;
+          done = true;
+          break;
+        }
         hl[d] = MV_PENDING;
         GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, d,
                                                     e.mv_q[d & 1]));
         hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, d, e.mv_q[(d + 1) & 1]);
         if (d >= dl + lag) {
           uint32_t x = 0;
-          if ((r = mv_wait(hl + (d - lag), e.st, x))) return r;
+          e.bfs_level = d - lag;
+        if ((r = mv_wait(hl + (d - lag), e.st, x))) return r;
           if (x == 0) { nlev = d + 1; done = true; break; }
           if (x <= a.small) { ++d; break; }  // levels d - 1, d are enqueued; small levels from d + 1
         }

@@ -152,6 +152,14 @@ int gs_device_count(int* n) {
   return GS_OK;
 }
 
+// Prune records a partition rank stages per round: past S * N / (2K) records per rank the
+// dense words (S * N u32, all-reduced) are the smaller exchange anyway.
+static size_t part_record_cap(size_t N, size_t S, uint32_t K) {
+  if (const char* x = std::getenv("GS_PART_RECORD_CAP"))  // (tests: the record exchange through a prune wave)
+    return std::max<size_t>(1, std::strtoull(x, nullptr, 10));
+  return std::max<size_t>(1u << 16, (S * N) / (2 * (size_t)K));
+}
+
 // K == 1: an engine over all nodes; K > 1: rank `rank` of a node-range partition.
 static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t n_slots, uint32_t rank,
                          uint32_t K, gs_engine** out) {
@@ -363,8 +371,8 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   e->sum_cap = (uint32_t)std::max<size_t>(64, std::min<size_t>(4096, (256ull << 20) / (S * sizeof(gs_round_summary))));
   ALLOC(e->sum, (size_t)e->sum_cap * S, 0);
   ALLOC(e->err, 4, 0);
-  if (e->part_on) {  // prune records of a round (the buffer grows in a prune wave)
-    e->part_rec_cap = std::max<size_t>(1u << 16, PAIRS);
+  if (e->part_on) {  // prune records of a round: when a round has more, its exchange is dense (gs_part_exchange_sizes)
+    e->part_rec_cap = part_record_cap(N, S, K);
     const size_t b1 = e->dev_bytes;
     ALLOC(e->part_rec, e->part_rec_cap, 0);
     e->pair_bytes += e->dev_bytes - b1;
@@ -603,6 +611,16 @@ static int refuse_part(Engine* e) {
   return e->part_on ? fail(GS_ESTATE, "a node-range partition rank runs rounds with gs_part_round") : GS_OK;
 }
 
+// Maps a BFS launcher's result: depth beyond u8 hops, a level that never finished, HIP errors.
+static int bfs_result(Engine* e, hipError_t r, const char* what) {
+  if (r == hipSuccess) return GS_OK;
+  if (r == hipErrorNotSupported) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
+  if (r == hipErrorLaunchTimeOut)
+    return fail(GS_EHIP, std::string(what) + ": BFS level " + std::to_string(e->bfs_level) +
+                             " did not finish within GS_LEVEL_WAIT_S (default 60 s); the device is stuck");
+  return fail(GS_EHIP, std::string(what) + ": " + hipGetErrorString(r));
+}
+
 static int do_bfs(Engine* e, bool record) {
   if (int s = refuse_part(e)) return s;
   if (int s = ensure_inb(e)) return s;
@@ -612,9 +630,7 @@ static int do_bfs(Engine* e, bool record) {
   hipError_t r = launch_bfs(*e, record);
   if (!self_timed) e->tend("bfs", t0);
   e->inb_valid = true;
-  if (r == hipErrorNotSupported) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
-  HIPC(r);
-  return GS_OK;
+  return bfs_result(e, r, "launch_bfs");
 }
 
 int gs_run_gossip(gs_engine* eh) {
@@ -705,8 +721,7 @@ int gs_round(gs_engine* eh, uint32_t round, int record) {
   if (e->bfs_mode == GS_BFS_MULTI && e->mv_fused) {  // gather fused with consume: the inbound rows stay on-chip
     hipError_t r = launch_bfs_multi(*e, rec, true);
     e->inb_valid = false;
-    if (r == hipErrorNotSupported) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
-    HIPC(r);
+    if (int s = bfs_result(e, r, "launch_bfs_multi")) return s;
     hipEvent_t t0;
     e->tbegin("consume", &t0);
     r = hipMemsetAsync(e->slot_prunes, 0, e->S * 4, e->st);
@@ -1172,8 +1187,7 @@ int gs_part_round(gs_engine* eh, uint32_t round, int record, uint32_t* n_records
   HIPC(hipMemsetAsync(e->part_cnt, 0, 4, e->st));
   hipError_t r = launch_bfs_multi(*e, rec, true);  // the whole BFS; gather + consume of own nodes
   e->inb_valid = false;
-  if (r == hipErrorNotSupported) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
-  HIPC(r);
+  if (int s = bfs_result(e, r, "launch_bfs_multi")) return s;
   hipEvent_t t0;
   e->tbegin("consume", &t0);
   r = hipMemsetAsync(e->slot_prunes, 0, e->S * 4, e->st);
@@ -1184,28 +1198,23 @@ int gs_part_round(gs_engine* eh, uint32_t round, int record, uint32_t* n_records
   HIPC(hipMemcpyAsync(e->h_err + 1, e->part_cnt, 4, hipMemcpyDeviceToHost, e->st));
   HIPC(hipStreamSynchronize(e->st));
   if (int s = check_err(e)) return s;
-  if (e->h_err[1] > e->part_rec_cap) {  // a prune wave: grow the record buffer and emit again
-    const size_t cap = (size_t)e->h_err[1] + e->h_err[1] / 4;
-    uint2* nb = nullptr;
-    HIPC(hipMalloc(&nb, cap * 8));
-    for (auto& p : e->allocs)
-      if (p == e->part_rec) { hipFree(p); p = nb; }
-    e->pair_bytes += (cap - e->part_rec_cap) * 8;
-    e->dev_bytes += (cap - e->part_rec_cap) * 8;
-    e->part_rec = nb;
-    e->part_rec_cap = cap;
-    HIPC(hipMemsetAsync(e->part_cnt, 0, 4, e->st));
-    HIPC(launch_part_emit(*e));
-    HIPC(hipMemcpyAsync(e->h_err + 1, e->part_cnt, 4, hipMemcpyDeviceToHost, e->st));
-    HIPC(hipStreamSynchronize(e->st));
-  }
-  e->part_nrec = e->h_err[1];
+  e->part_nrec = e->h_err[1];  // (more than part_rec_cap: only the dense exchange can carry this round)
   *n_records = e->part_nrec;
+  return GS_OK;
+}
+
+int gs_part_exchange_sizes(gs_engine* eh, size_t* record_cap, size_t* dense_words) {
+  PART(eh);
+  if (record_cap) *record_cap = e->part_rec_cap;
+  if (dense_words) *dense_words = (size_t)e->S * e->N;
   return GS_OK;
 }
 
 int gs_part_prunes_out(gs_engine* eh, void* dst, int dev) {
   PART(eh);
+  if (e->part_nrec > e->part_rec_cap)
+    return fail(GS_ERANGE, "this round's prune records exceed the record buffer: exchange them dense "
+                           "(gs_part_prunes_dense_out / _in)");
   if (e->part_nrec) HIPC(hipMemcpyAsync(dst, e->part_rec, (size_t)e->part_nrec * 8, kind_to(dev), e->st));
   HIPC(hipStreamSynchronize(e->st));
   return GS_OK;
@@ -1227,6 +1236,40 @@ int gs_part_prunes_in(gs_engine* eh, const void* src, size_t n, int dev) {
     rec = e->part_in;
   }
   HIPC(launch_part_prunes_apply(*e, rec, n));
+  HIPC(hipStreamSynchronize(e->st));
+  return check_err(e);
+}
+
+int gs_part_prunes_dense_out(gs_engine* eh, void* dst, int dev) {
+  PART(eh);
+  if (!dst) return fail(GS_EINVAL, "null argument");
+  uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+  if (!dev) {  // host buffer: staged in a device buffer of the same size
+    if (!e->part_dense) {
+      const int s = dalloc(*e, &e->part_dense, (size_t)e->S * e->N, 0);
+      if (s) return s;
+    }
+    d = e->part_dense;
+  }
+  HIPC(launch_part_emit_dense(*e, d));
+  if (!dev) HIPC(hipMemcpyAsync(dst, d, (size_t)e->S * e->N * 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_part_prunes_dense_in(gs_engine* eh, const void* src, int dev) {
+  PART(eh);
+  if (!src) return fail(GS_EINVAL, "null argument");
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(src);
+  if (!dev) {
+    if (!e->part_dense) {
+      const int s = dalloc(*e, &e->part_dense, (size_t)e->S * e->N, 0);
+      if (s) return s;
+    }
+    HIPC(hipMemcpyAsync(e->part_dense, src, (size_t)e->S * e->N * 4, hipMemcpyHostToDevice, e->st));
+    d = e->part_dense;
+  }
+  HIPC(launch_part_dense_apply(*e, d));
   HIPC(hipStreamSynchronize(e->st));
   return check_err(e);
 }

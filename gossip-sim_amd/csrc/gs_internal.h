@@ -125,6 +125,7 @@ struct Engine {
   uint2* mv_seed = nullptr;       // [S] seed entries (distinct origins) of every group
   std::vector<MvGroup> mv_groups;
   bool mv_attr_set = false;
+  uint32_t bfs_level = 0;  // the level loop's current level (reported when a level wait times out)
   bool mv_diag = false;  // GS_MV_DIAG=1
   bool mv_line = false;   // multi: prune masks live in the row table's node lines (msu = 32)
   bool mv_fused = false;  // gs_round: gather, then k_cg_consume; GS_MV_FUSED=1: fused gather + consume (slower at C4)
@@ -142,8 +143,9 @@ struct Engine {
   // (= [vlo, vlo + NP)) and the fine bins [part_flo, part_flo + part_fno) of the multi BFS
   bool part_on = false;
   uint32_t part_rank = 0, part_K = 1, part_lo = 0, part_hi = 0, part_flo = 0, part_fno = 0;
-  uint2* part_rec = nullptr;        // prune records of this rank's round: (slot * N + prunee, ring bits), grow-only
-  size_t part_rec_cap = 0;
+  uint2* part_rec = nullptr;        // prune records of this rank's round: (slot * N + prunee, ring bits)
+  size_t part_rec_cap = 0;          // fixed at create (beyond it the round's exchange is dense)
+  uint32_t* part_dense = nullptr;   // [N][S] dense prune words (allocated on the first dense host exchange)
   uint32_t* part_cnt = nullptr;     // [1]: prune records staged
   uint32_t part_nrec = 0;           // records of the last gs_part_round
   uint2* part_in = nullptr;         // every rank's prune records (gs_part_prunes_in), grow-only
@@ -200,7 +202,9 @@ hipError_t launch_bfs_binned(Engine& e, bool record);
 // spin on a host-mapped word the device writes (MV_PENDING until then); checks the stream
 // now and then so a stream that ended without writing it fails instead of hanging
 constexpr uint32_t MV_PENDING = 0xFFFFFFFFu;
-hipError_t mv_wait(volatile uint32_t* p, hipStream_t st, uint32_t& out);
+hipError_t mv_wait(volatile uint32_t* p, hipStream_t st, uint32_t& out);  // bounded: hipErrorLaunchTimeOut
+// after the level loop enqueued levels through d - 1: is level d's frontier empty (syncs the stream)
+hipError_t level_empty(Engine& e, uint32_t d, bool& empty);
 hipError_t launch_bfs_level_step(Engine& e, bool record, uint32_t d, uint32_t qmin, uint32_t qmax);
 void bin_geometry(uint32_t N, size_t PAIRS, uint32_t fcap, BinGeom& g, bool allow_narrow);
 bool bin_supported(const BinGeom& g, uint32_t fcap);
@@ -223,6 +227,8 @@ hipError_t launch_part_stats_pack(Engine& e);
 hipError_t launch_part_stats_unpack(Engine& e);
 hipError_t launch_part_prunes_apply(Engine& e, const uint2* rec, size_t n);
 hipError_t launch_part_emit(Engine& e);  // this round's prune records -> part_rec (count in part_cnt)
+hipError_t launch_part_emit_dense(Engine& e, uint32_t* dense);         // ... as dense words [N][S] (zeroed first)
+hipError_t launch_part_dense_apply(Engine& e, const uint32_t* dense);  // masks |= the summed dense words
 // Rotation of round `round` (decide + entries); the prune-bit clear of the replaced
 // ring slots runs now, or with defer_clear it is left pending for the next one-kernel
 // round (which applies it to its LDS copy of the masks) or launch_rotate_clear.

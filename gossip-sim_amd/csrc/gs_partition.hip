@@ -14,7 +14,9 @@
 // (gossip.rs:618-653) and runs send_prunes for its own pruners (gossip.rs:657-699).
 // prune_connections (gossip.rs:701-737) sets bits in the PRUNEE's replicated mask row:
 // each rank stages its prunes as records (slot * N + prunee, ring-slot bits), the
-// ranks all-gather them and every rank ORs every record into its masks. Recorded
+// ranks all-gather them and every rank ORs every record into its masks -- or, when the
+// records outgrow the preallocated buffer or the dense form is smaller (a prune wave),
+// as dense bit words [N][S] that the ranks SUM-all-reduce (bit-disjoint, so SUM = OR). Recorded
 // statistics are partial sums over owned nodes (counts, hop bins, the stranded bitmap
 // over stake rank), summed over ranks before the per-slot summary is finalized. The
 // exchanges are the caller's (RCCL on device buffers, or host buffers): see
@@ -114,6 +116,54 @@ __global__ __launch_bounds__(256) void k_part_emit(const uint8_t* __restrict__ p
   }
 }
 
+// The same prunes as dense words: dense[u * S + o] |= the ring-slot bits of prunee u's
+// entry for slot o (the caller zeroed dense). Every (slot, prunee) word gets bits from
+// pruners of one rank only per ring slot -- a ring slot holds one pruner, and a pruner is
+// owned by one rank -- so the ranks' words are bit-disjoint and their SUM is their OR.
+template <int ASZP>
+__global__ __launch_bounds__(256) void k_part_emit_dense(const uint8_t* __restrict__ prune_round,
+                                                         const uint32_t* __restrict__ cmeta,
+                                                         const uint32_t* __restrict__ ckey,
+                                                         const uint8_t* __restrict__ bucket,
+                                                         const uint8_t* __restrict__ obkt,
+                                                         const uint32_t* __restrict__ peers,
+                                                         const uint16_t* __restrict__ hl, uint32_t S, uint32_t NP,
+                                                         uint32_t vlo, uint32_t ASZ, size_t PAIRS,
+                                                         uint32_t* __restrict__ dense) {
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < PAIRS; q += (size_t)gridDim.x * blockDim.x) {
+    if (!prune_round[q]) continue;
+    const uint32_t o = (uint32_t)(q / NP), v = vlo + (uint32_t)(q - (size_t)o * NP);
+    const uint32_t plen = (cmeta[q] >> 16) & 0xFFu, ob = obkt[o];
+    for (uint32_t i = 0; i < plen; ++i) {
+      const uint32_t w = ckey[(size_t)i * PAIRS + q];
+      if (!ck_pruned(w)) continue;
+      const uint32_t u = ck_id(w);
+      const uint32_t ent = u * NB + min((uint32_t)bucket[u], ob);
+      const uint32_t hv = hl[ent], head = hv & 0xFF, L = hv >> 8;
+      uint32_t row[ASZP];
+      load_row<ASZP>(peers + (size_t)ent * ASZP, row);
+      uint32_t hit = 0;
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        const uint32_t pos = (uint32_t)s >= head ? (uint32_t)s - head : (uint32_t)s + ASZ - head;
+        hit |= (uint32_t)((uint32_t)s < ASZ && pos < L && row[s] == v) << s;
+      }
+      if (hit) atomicOr(&dense[(size_t)u * S + o], hit);
+    }
+  }
+}
+
+// prune_connections from the summed dense words: mask |= word (push_active_set.rs:56-71).
+__global__ void k_part_dense_apply(uint32_t* mask, size_t mso, size_t msu, uint32_t S, size_t words,
+                                   const uint32_t* __restrict__ dense) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t x = dense[i];
+    if (!x) continue;
+    const size_t u = i / S, o = i - u * S;
+    mask[o * mso + u * msu] |= x;  // (one thread per word: no atomic needed)
+  }
+}
+
 uint32_t grid_of(size_t n, uint32_t cap = 4096) {
   const size_t g = (n + 255) / 256;
   return (uint32_t)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -139,6 +189,22 @@ hipError_t launch_part_emit(Engine& e) {
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_part_emit<A>, dim3(grid_of(e.PAIRS, 8192)), dim3(256), 0, e.st,
                                               e.prune_round, e.cmeta, e.ckey, e.bucket, e.obkt, e.peers, e.hl, e.N,
                                               e.NP, e.vlo, e.ASZ, e.PAIRS, e.part_rec, e.part_rec_cap, e.part_cnt));
+  return hipGetLastError();
+}
+
+hipError_t launch_part_emit_dense(Engine& e, uint32_t* dense) {
+  hipError_t r = hipMemsetAsync(dense, 0, (size_t)e.S * e.N * 4, e.st);
+  if (r != hipSuccess) return r;
+  GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_part_emit_dense<A>, dim3(grid_of(e.PAIRS, 8192)), dim3(256), 0, e.st,
+                                              e.prune_round, e.cmeta, e.ckey, e.bucket, e.obkt, e.peers, e.hl, e.S,
+                                              e.NP, e.vlo, e.ASZ, e.PAIRS, dense));
+  return hipGetLastError();
+}
+
+hipError_t launch_part_dense_apply(Engine& e, const uint32_t* dense) {
+  const size_t words = (size_t)e.S * e.N;
+  hipLaunchKernelGGL(k_part_dense_apply, dim3(grid_of(words, 8192)), dim3(256), 0, e.st, e.mask, e.mso, e.msu, e.S,
+                     words, dense);
   return hipGetLastError();
 }
 

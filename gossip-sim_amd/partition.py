@@ -7,10 +7,14 @@ nodes only. Active-set rows, prune masks and failed flags are replicated. A roun
 call sequence of include/gossip_hip.h gs_part_*; this class runs it and does the
 exchanges with torch.distributed:
 
-  after consume   all-gather of the ranks' prune-record counts, then of the records
-                  (padded to the largest count); every rank applies every record
-                  (prune_connections on the replicated masks). Nothing is exchanged
-                  per BFS level: each rank runs the whole BFS over its replicated rows.
+  after consume   all-gather of the ranks' prune-record counts; then, the same choice
+                  on every rank, either an all-gather of the records (padded to the
+                  largest count; every rank applies every record) or -- when a rank's
+                  records overflow its preallocated buffer or the dense form is smaller,
+                  as in a prune wave -- a SUM all-reduce of dense [N][S] ring-slot bit
+                  words (bit-disjoint across ranks, so SUM = OR). Either way this is
+                  prune_connections on the replicated masks. Nothing is exchanged per BFS
+                  level: each rank runs the whole BFS over its replicated rows.
   recorded round  SUM of the statistics partials (u64 words).
 
 With the "nccl" backend (RCCL over xGMI) the exchange buffers are torch tensors on the
@@ -25,14 +29,28 @@ import numpy as np
 from . import GS_BFS_MULTI, Engine, _check, lib
 
 
+def partition_ranges(n, world):
+    """The node ranges gs_create_part gives ranks 0..world-1: contiguous, whole 1,024-id
+    bins of ceil(n / world) rounded up. Raises ValueError when a trailing rank would own
+    no node (e.g. n = 3,000 over 4 ranks) -- identically on every rank, before any engine
+    or collective exists, so no rank is left waiting in a collective."""
+    c = ((-(-n // world)) + 1023) & ~1023
+    out = [(min(n, r * c), min(n, r * c + c)) for r in range(world)]
+    if any(lo >= hi for lo, hi in out):
+        raise ValueError(f"a node-range partition of {n} nodes over {world} ranks leaves a rank without nodes "
+                         f"(ranges are whole 1,024-id bins of {c}); use at most {-(-n // c)} ranks")
+    return out
+
+
 class PartitionedEngine:
-    def __init__(self, stakes, n_slots, *, group=None, device=0, **engine_kw):
+    def __init__(self, stakes, n_slots, *, group=None, device=0, exchange="auto", **engine_kw):
         import torch
         import torch.distributed as tdist
         self.torch, self.tdist, self.group = torch, tdist, group
         self.rank = tdist.get_rank(group)
         self.world = tdist.get_world_size(group)
         engine_kw["bfs_mode"] = GS_BFS_MULTI
+        partition_ranges(len(stakes), self.world)  # (raises the same on every rank)
         self.eng = Engine(stakes, n_slots, device=device, part=(self.rank, self.world), **engine_kw)
         sw = C.c_size_t()
         lo, hi = C.c_uint32(), C.c_uint32()
@@ -43,7 +61,16 @@ class PartitionedEngine:
             torch.cuda.set_device(device)
         self.dev = torch.device("cuda", device) if self.on_device else torch.device("cpu")
         self.stats = torch.zeros(sw.value, dtype=torch.int64, device=self.dev)
-        self.records = 0  # prune records exchanged in the last round (all ranks)
+        rc, dw = C.c_size_t(), C.c_size_t()
+        _check(lib().gs_part_exchange_sizes(self.eng.h, C.byref(rc), C.byref(dw)))
+        self.record_cap, self.dense_words = rc.value, dw.value
+        if exchange not in ("auto", "records", "dense"):
+            raise ValueError("exchange must be auto, records or dense")
+        self.exchange = exchange
+        self.dense = None      # [N * S] int32 exchange buffer, allocated on the first dense round
+        self.records = 0       # prune records of the last round (all ranks)
+        self.last_mode = None  # "records" / "dense" / None (no prunes)
+        self.bytes_in = 0      # exchange bytes this rank received over all rounds (collective payload)
 
     # the Engine's other calls (set_slots, init_active_sets, fail_nodes, readbacks) are
     # replicated or rank-local and need no exchange
@@ -67,15 +94,36 @@ class PartitionedEngine:
         tdist.all_gather(counts, torch.tensor([n.value], dtype=torch.int64, device=self.dev), group=self.group)
         counts = [int(c.item()) for c in counts]
         m = max(counts)
+        self.last_mode = None
         if m:
-            mine = torch.zeros(2 * m, dtype=torch.int32, device=self.dev)
-            if n.value:
-                _check(L.gs_part_prunes_out(h, self._ptr(mine), dev))
-            parts = [torch.zeros(2 * m, dtype=torch.int32, device=self.dev) for _ in range(self.world)]
-            tdist.all_gather(parts, mine, group=self.group)
-            recs = torch.cat([p[:2 * c] for p, c in zip(parts, counts)])
-            self._done()
-            _check(L.gs_part_prunes_in(h, self._ptr(recs), sum(counts), dev))
+            # records: every rank receives world * m padded records (8 B); dense: a ring
+            # all-reduce moves ~2 x the S * N words (4 B) through every rank
+            rec_bytes, dense_bytes = 8 * m * self.world, 8 * self.dense_words
+            dense = self.exchange == "dense" or (self.exchange == "auto" and
+                                                 (m > self.record_cap or rec_bytes > dense_bytes))
+            if not dense and m > self.record_cap:
+                raise RuntimeError(f"{m} prune records exceed the record buffer ({self.record_cap}); "
+                                   "use exchange='auto' or 'dense'")
+            if dense:
+                if self.dense is None:
+                    self.dense = torch.zeros(self.dense_words, dtype=torch.int32, device=self.dev)
+                _check(L.gs_part_prunes_dense_out(h, self._ptr(self.dense), dev))
+                tdist.all_reduce(self.dense, group=self.group)
+                self._done()
+                _check(L.gs_part_prunes_dense_in(h, self._ptr(self.dense), dev))
+                self.bytes_in += dense_bytes
+                self.last_mode = "dense"
+            else:
+                mine = torch.zeros(2 * m, dtype=torch.int32, device=self.dev)
+                if n.value:
+                    _check(L.gs_part_prunes_out(h, self._ptr(mine), dev))
+                parts = [torch.zeros(2 * m, dtype=torch.int32, device=self.dev) for _ in range(self.world)]
+                tdist.all_gather(parts, mine, group=self.group)
+                recs = torch.cat([p[:2 * c] for p, c in zip(parts, counts)])
+                self._done()
+                _check(L.gs_part_prunes_in(h, self._ptr(recs), sum(counts), dev))
+                self.bytes_in += rec_bytes
+                self.last_mode = "records"
         self.records = sum(counts)
         self.eng.chance_to_rotate(round_index)
         if record:

@@ -57,7 +57,7 @@ enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24
  * else LEVEL. */
 enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2, GS_BFS_BINNED = 3, GS_BFS_MULTI = 4 };
 enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4, GS_FLAG_BINNED_ALL_LEVELS = 8,
-       GS_FLAG_WIDE_RECORDS = 16 };
+       GS_FLAG_WIDE_RECORDS = 16, GS_FLAG_NO_SMALL_LEVELS = 32 };
 
 typedef struct gs_params {
   uint32_t push_fanout;         /* Config::gossip_push_fanout (gossip.rs:113) */
@@ -79,7 +79,10 @@ typedef struct gs_params {
                                    GS_FLAG_BINNED_ALL_LEVELS: GS_BFS_BINNED bins every level, not
                                    only levels with >= 2^17 frontier pairs (same results);
                                    GS_FLAG_WIDE_RECORDS: GS_BFS_BINNED keeps 8-byte push records
-                                   even where 4-byte ones fit (same results) */
+                                   even where 4-byte ones fit (same results);
+                                   GS_FLAG_NO_SMALL_LEVELS: GS_BFS_BINNED / GS_BFS_MULTI run no level
+                                   in their single-workgroup small-level kernels (every level
+                                   through the grid-wide kernels; same results) */
 } gs_params;
 
 typedef struct gs_slot {
@@ -185,7 +188,9 @@ int gs_engine_round_kind(gs_engine* e, uint32_t* fused);
 /* --- node-range partition ------------------------------
  * K engines, one per rank/GPU, created with gs_create_part on the same stakes, params
  * (bfs_mode GS_BFS_MULTI or AUTO), slots and seed. Rank r owns the node ids
- * [node_lo, node_hi) (gs_part_sizes): K contiguous ranges of whole 1,024-id bins.
+ * [node_lo, node_hi) (gs_part_sizes): K contiguous ranges of whole 1,024-id bins of
+ * C = ceil(n / K) rounded up to 1,024; every rank must own a node ((K - 1) * C < n, else
+ * gs_create_part fails with GS_EINVAL on the empty ranks -- check before creating).
  * Replicated on every rank: active sets, prune masks, failed flags (the same rotations,
  * failures and prune bits are applied everywhere). Kept for owned nodes only: every
  * per-(slot, node) array -- hops, in-degrees, received caches, round counters,
@@ -193,8 +198,12 @@ int gs_engine_round_kind(gs_engine* e, uint32_t* fused);
  * its replicated tables (no exchange per level) and gathers, consumes and prunes for
  * its own nodes. One iteration of gossip_main.rs:449-564 is:
  *   gs_part_round(round, record, &n)        run_gossip + consume + send_prunes; n prune records
- *   ALL-GATHER the ranks' records (gs_part_prunes_out, n x 2 u32 words: slot * n_nodes +
- *       prunee, ring-slot bits) -> gs_part_prunes_in(all records)   prune_connections
+ *   ALL-GATHER the n's, then prune_connections by ONE of (every rank picks the same):
+ *     records: ALL-GATHER the ranks' records (gs_part_prunes_out, n x 2 u32 words: slot *
+ *       n_nodes + prunee, ring-slot bits) -> gs_part_prunes_in(all records); only while
+ *       every n <= record_cap (gs_part_exchange_sizes) and the records are the smaller form;
+ *     dense: gs_part_prunes_dense_out (dense_words u32 = [n_nodes][n_slots] ring-slot bits)
+ *       -> SUM ALL-REDUCE (the ranks' bits are disjoint: SUM = OR) -> gs_part_prunes_dense_in;
  *   gs_chance_to_rotate(round);
  *   if recorded: gs_part_stats_out -> SUM over ranks -> gs_part_stats_in.
  * The exchanges are the caller's: RCCL on device buffers over xGMI, or host buffers
@@ -208,6 +217,9 @@ int gs_part_sizes(gs_engine* e, size_t* stats_words, uint32_t* node_lo, uint32_t
 int gs_part_round(gs_engine* e, uint32_t round, int record, uint32_t* n_records);
 int gs_part_prunes_out(gs_engine* e, void* dst, int dst_device);                 /* [n_records][2] u32 */
 int gs_part_prunes_in(gs_engine* e, const void* src, size_t n_records, int src_device);
+int gs_part_exchange_sizes(gs_engine* e, size_t* record_cap, size_t* dense_words);
+int gs_part_prunes_dense_out(gs_engine* e, void* dst, int dst_device);           /* [n_nodes][n_slots] u32 */
+int gs_part_prunes_dense_in(gs_engine* e, const void* src, int src_device);
 int gs_part_stats_out(gs_engine* e, void* dst, int dst_device);          /* [S][5 + 256 + W] u64 */
 int gs_part_stats_in(gs_engine* e, const void* src, int src_device);
 

@@ -94,9 +94,9 @@ void or_entry_prune(void* e, const uint8_t* node, const uint8_t* origin) {
 }
 int or_entry_filter_contains(void* e, const uint8_t* node, const uint8_t* key) {
   auto* en = (PushActiveSetEntry*)e;
-  auto it = en->filters.find(pk_at(node));
-  if (it == en->filters.end()) return -1;
-  return it->second.count(pk_at(key)) ? 1 : 0;
+  const long i = en->index_of(pk_at(node));
+  if (i < 0) return -1;
+  return en->filter_contains((size_t)i, pk_at(key)) ? 1 : 0;
 }
 
 // ------------------------------------------------------ PushActiveSet ----
@@ -296,7 +296,7 @@ void or_sim_pruned_all(void* sp, size_t origin, uint32_t* out) {
     auto& e = s->nodes[n].active_set.e[get_stake_bucket(m)];
     uint32_t bits = 0;
     for (size_t i = 0; i < e.keys.size(); ++i)
-      if (e.keys[i] != o && e.filters.at(e.keys[i]).count(o)) bits |= 1u << i;
+      if (e.keys[i] != o && e.filter_contains(i, o)) bits |= 1u << i;
     out[n] = bits;
   }
 }
@@ -323,10 +323,10 @@ void or_sim_caches(void* sp, size_t origin, uint32_t* up, uint32_t* len, uint32_
 // 1 if `origin` is in the filter of `peer` inside entry k of `node` (prune state).
 int or_sim_entry_pruned(void* sp, size_t node, int k, size_t peer, size_t origin) {
   Sim* s = (Sim*)sp;
-  auto& f = s->nodes[node].active_set.e[k].filters;
-  auto it = f.find(s->nodes[peer].pk);
-  if (it == f.end()) return -1;
-  return it->second.count(s->nodes[origin].pk) ? 1 : 0;
+  auto& en = s->nodes[node].active_set.e[k];
+  const long i = en.index_of(s->nodes[peer].pk);
+  if (i < 0) return -1;
+  return en.filter_contains((size_t)i, s->nodes[origin].pk) ? 1 : 0;
 }
 long or_sim_cache(void* sp, size_t node, size_t origin, uint64_t* upserts, uint32_t* keys, uint64_t* scores,
                   size_t cap) {
@@ -346,6 +346,115 @@ void or_sim_failed(void* sp, uint8_t* out) {
   for (size_t i = 0; i < s->nodes.size(); ++i) out[i] = s->nodes[i].failed;
 }
 size_t or_sim_total_prunes(void* s) { return ((Sim*)s)->cluster.total_prunes; }
+
+// Bulk upload of every node's active set (the engine's, for checks at sizes where the
+// reference's O(25 N^2) initialize_gossip cannot run): entry k of node n gets the peers
+// peers[(n*25+k)*cap + i], i < len[n*25+k], in FIFO order, each with a fresh filter
+// (only the key itself), as PushActiveSetEntry::rotate leaves a newly inserted key
+// (push_active_set.rs:171-180). Indices are the caller's node indices.
+int or_sim_set_entries(void* sp, const uint32_t* peers, const uint8_t* len, size_t cap) {
+  Sim* s = (Sim*)sp;
+  const size_t n = s->nodes.size();
+  for (size_t v = 0; v < n; ++v)
+    for (int k = 0; k < NUM_PUSH_ACTIVE_SET_ENTRIES; ++k) {
+      auto& e = s->nodes[v].active_set.e[k];
+      const size_t L = len[v * 25 + k];
+      if (L > cap) { g_err = "entry longer than cap"; return -1; }
+      e.keys.clear();
+      e.keys.shrink_to_fit();
+      e.keys.reserve(L);
+      e.pruned.clear();
+      for (size_t i = 0; i < L; ++i) {
+        const uint32_t p = peers[(v * 25 + k) * cap + i];
+        if (p >= n || p == v) { g_err = "bad peer index"; return -1; }
+        e.keys.push_back(s->nodes[p].pk);
+      }
+    }
+  return 0;
+}
+
+// Bulk orders (gossip.rs:601-607) of every destination as CSR in caller-index order:
+// off[n + 1]; each list in consume order (hop, then base58 rank) as or_sim_orders.
+// Returns the record count, or -1 when it exceeds cap (nothing written past cap).
+long or_sim_orders_all(void* sp, uint32_t* off, uint32_t* src, uint8_t* hop, size_t cap) {
+  Sim* s = (Sim*)sp;
+  size_t w = 0;
+  off[0] = 0;
+  std::vector<std::pair<uint64_t, uint64_t>> v;
+  for (size_t d = 0; d < s->nodes.size(); ++d) {
+    auto it = s->cluster.orders.find(s->nodes[d].pk);
+    if (it != s->cluster.orders.end()) {
+      v.clear();
+      for (auto& kv : it->second) v.push_back({kv.second, s->rank.at(kv.first)});
+      std::sort(v.begin(), v.end());
+      if (w + v.size() > cap) return -1;
+      for (auto& pr : v) {
+        src[w] = (uint32_t)s->index.at(s->by_rank[pr.second]);
+        hop[w] = (uint8_t)std::min<uint64_t>(pr.first, 255);
+        ++w;
+      }
+    }
+    off[d + 1] = (uint32_t)w;
+  }
+  return (long)w;
+}
+
+// One node's active set after initialize_gossip and `rounds` chance_to_rotate calls in
+// PHILOX mode, replayed for that node alone: the determinism contract makes a node's
+// entries a function of (seed, its id, the rounds) only. Nodes are ids 0..n-1 (the id
+// order is the candidate order); their pubkeys are stand-ins (only equality matters).
+// Follows Sim::init_philox / Sim::chance_to_rotate (gossip.rs:739-754, 805-842,
+// push_active_set.rs:153-187). Writes peers[k*cap + i] (ids, FIFO order) and len[k];
+// returns the number of rotations the node made, -1 on a bad argument.
+long or_replay_node_entries(uint64_t seed, const uint64_t* stakes_by_id, size_t n, size_t node, size_t asz,
+                            double p, uint32_t rounds, uint32_t* peers, uint8_t* len, size_t cap) {
+  if (node >= n || asz > cap) { g_err = "bad argument"; return -1; }
+  auto pk = [](size_t i) {
+    Pubkey k{};
+    for (int b = 0; b < 8; ++b) k.b[31 - b] = (uint8_t)(i >> (8 * b));
+    k.b[0] = 0xA5;  // never all-zero
+    return k;
+  };
+  Stakes st;
+  st.reserve(n);
+  std::vector<Pubkey> cand;
+  cand.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    st[pk(i)] = stakes_by_id[i];
+    if (i != node) cand.push_back(pk(i));
+  }
+  PushActiveSet as;
+  const uint32_t id = (uint32_t)node;
+  {
+    std::vector<PhiloxStream> streams;
+    for (int k = 0; k < NUM_PUSH_ACTIVE_SET_ENTRIES; ++k) streams.emplace_back(seed, P_INIT, id, (uint32_t)k);
+    as.rotate([&](int k) -> Rng& { return streams[k]; }, asz, cand, st);
+  }
+  long rot = 0;
+  for (uint32_t r = 0; r < rounds; ++r) {
+    PhiloxStream dec(seed, P_DECIDE, id, r);
+    if (gen_f64(dec) < p) {
+      std::vector<PhiloxStream> streams;
+      for (int k = 0; k < NUM_PUSH_ACTIVE_SET_ENTRIES; ++k)
+        streams.emplace_back(seed, P_ROTATE, id, (r << 5) | (uint32_t)k);
+      as.rotate([&](int k) -> Rng& { return streams[k]; }, asz, cand, st);
+      ++rot;
+    }
+  }
+  for (int k = 0; k < NUM_PUSH_ACTIVE_SET_ENTRIES; ++k) {
+    const auto& keys = as.e[k].keys;
+    len[k] = (uint8_t)keys.size();
+    for (size_t i = 0; i < cap; ++i) {
+      uint32_t v = 0xFFFFFFFFu;
+      if (i < keys.size()) {
+        v = 0;
+        for (int b = 0; b < 8; ++b) v |= (uint32_t)keys[i].b[31 - b] << (8 * b);  // ids < 2^32
+      }
+      peers[(size_t)k * cap + i] = v;
+    }
+  }
+  return rot;
+}
 
 // --------------------------------------------------------------- stats ----
 void* or_stats_new() { return new StatsHandle(); }

@@ -171,19 +171,30 @@ std::optional<size_t> WeightedShuffle::next(Rng& rng) {
 }
 
 // --------------------------------------------------- PushActiveSet ----
+long PushActiveSetEntry::index_of(const Pubkey& node) const {
+  for (size_t i = 0; i < keys.size(); ++i)
+    if (keys[i] == node) return (long)i;
+  return -1;
+}
+
+bool PushActiveSetEntry::filter_contains(size_t i, const Pubkey& x) const {
+  if (x == keys[i]) return true;
+  for (const auto& pr : pruned)
+    if (pr.first == i && pr.second == x) return true;
+  return false;
+}
+
 std::vector<Pubkey> PushActiveSetEntry::get_nodes(const Pubkey& origin,
                                                   const std::function<bool(const Pubkey&)>& force) const {
   std::vector<Pubkey> out;
-  for (const auto& k : keys) {
-    const auto& f = filters.at(k);
-    if (!f.count(origin) || force(k)) out.push_back(k);
-  }
+  for (size_t i = 0; i < keys.size(); ++i)
+    if (!filter_contains(i, origin) || force(keys[i])) out.push_back(keys[i]);
   return out;
 }
 
 void PushActiveSetEntry::prune(const Pubkey& node, const Pubkey& origin) {
-  auto it = filters.find(node);
-  if (it != filters.end()) it->second.insert(origin);
+  const long i = index_of(node);  // push_active_set.rs:56-71: only a present key's filter
+  if (i >= 0 && !filter_contains((size_t)i, origin)) pruned.push_back({(uint32_t)i, origin});
 }
 
 void PushActiveSetEntry::rotate(Rng& rng, size_t size, const std::vector<Pubkey>& nodes,
@@ -194,13 +205,15 @@ void PushActiveSetEntry::rotate(Rng& rng, size_t size, const std::vector<Pubkey>
     if (!k) break;
     if (keys.size() > size) break;
     const Pubkey& node = nodes[*k];
-    if (filters.count(node)) continue;
-    keys.push_back(node);
-    filters[node] = PkSet{node};  // bloom.add(node): a peer never receives its own origin
+    if (index_of(node) >= 0) continue;
+    keys.push_back(node);  // with a fresh filter holding the node itself: a peer never receives its own origin
   }
-  while (keys.size() > size) {  // shift_remove_index(0)
-    filters.erase(keys.front());
+  while (keys.size() > size) {  // shift_remove_index(0): the front key and its filter go, indices shift down
     keys.erase(keys.begin());
+    std::vector<std::pair<uint32_t, Pubkey>> kept;
+    for (const auto& pr : pruned)
+      if (pr.first > 0) kept.push_back({pr.first - 1, pr.second});
+    pruned.swap(kept);
   }
 }
 

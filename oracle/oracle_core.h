@@ -51,11 +51,16 @@ struct Pubkey {
   // solana_sdk::Pubkey derives Ord over its [u8; 32]: lexicographic bytes.
   bool operator<(const Pubkey& o) const { return std::memcmp(b, o.b, 32) < 0; }
 };
-struct PubkeyHash {
+struct PubkeyHash {  // (iteration order of these maps never decides a result: the reference's is random)
+  static uint64_t mix(uint64_t x) {  // splitmix64 finalizer
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27; x *= 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+  }
   size_t operator()(const Pubkey& p) const {
-    uint64_t h = 1469598103934665603ull;  // FNV-1a 64 over the 32 bytes
-    for (int i = 0; i < 32; ++i) { h ^= p.b[i]; h *= 1099511628211ull; }
-    return (size_t)h;
+    uint64_t w[4];
+    std::memcpy(w, p.b, 32);
+    return (size_t)mix(w[0] ^ mix(w[1] ^ mix(w[2] ^ mix(w[3]))));
   }
 };
 template <class V> using PkMap = std::unordered_map<Pubkey, V, PubkeyHash>;
@@ -136,7 +141,12 @@ struct WeightedShuffle {
 // ------------------------------------------------------- PushActiveSet ----
 struct PushActiveSetEntry {
   std::vector<Pubkey> keys;        // IndexMap insertion order
-  PkMap<PkSet> filters;            // exact stand-in for AtomicBloom<Pubkey>
+  // Exact stand-in for each key's AtomicBloom<Pubkey>: the key itself (bloom.add(node),
+  // push_active_set.rs:179) plus the origins pruned for it, kept as (key index, origin)
+  // pairs (a per-key set cost ~2 KB per entry, which 1M-node checks cannot afford).
+  std::vector<std::pair<uint32_t, Pubkey>> pruned;
+  long index_of(const Pubkey& node) const;  // IndexMap::get_index_of
+  bool filter_contains(size_t i, const Pubkey& x) const;
   std::vector<Pubkey> get_nodes(const Pubkey& origin, const std::function<bool(const Pubkey&)>& force) const;
   void prune(const Pubkey& node, const Pubkey& origin);
   void rotate(Rng& rng, size_t size, const std::vector<Pubkey>& nodes, const std::vector<uint64_t>& weights);

@@ -117,6 +117,9 @@ def _load():
         "or_sim_cache": (C.c_long, [P, SZ, SZ, P, P, P, SZ]),
         "or_sim_failed": (None, [P, P]),
         "or_sim_total_prunes": (SZ, [P]),
+        "or_sim_set_entries": (I, [P, P, P, SZ]),
+        "or_sim_orders_all": (C.c_long, [P, P, P, P, SZ]),
+        "or_replay_node_entries": (C.c_long, [U64, P, SZ, SZ, SZ, D, U32, P, P, SZ]),
         "or_stats_new": (P, []),
         "or_stats_free": (None, [P]),
         "or_stats_insert_hops": (None, [P, P, SZ]),
@@ -446,6 +449,35 @@ class Sim:
 
     def total_prunes(self):
         return lib.or_sim_total_prunes(self.h)
+
+    def set_entries(self, peers, lens):
+        """Every node's entries at once (peers [n, 25, cap] in FIFO order, lens [n, 25])."""
+        p = np.ascontiguousarray(peers, dtype=np.uint32)
+        ln = np.ascontiguousarray(lens, dtype=np.uint8)
+        if lib.or_sim_set_entries(self.h, _ptr(p), _ptr(ln), p.shape[2]) != 0:
+            raise ValueError(lib.or_last_error().decode())
+
+    def orders_all(self, cap):
+        """Every destination's orders as CSR (off [n+1], src, hop), lists in consume order."""
+        off = np.zeros(self.n + 1, dtype=np.uint32)
+        src = np.zeros(cap, dtype=np.uint32)
+        hop = np.zeros(cap, dtype=np.uint8)
+        c = lib.or_sim_orders_all(self.h, _ptr(off), _ptr(src), _ptr(hop), cap)
+        if c < 0:
+            raise ValueError("orders exceed cap")
+        return off, src[:c], hop[:c]
+
+
+def replay_node_entries(seed, stakes, node, asz, p, rounds):
+    """One node's entries after init + `rounds` rotation rounds (PHILOX), replayed alone:
+    (peers [25, asz] ids in FIFO order, lens [25], rotations made)."""
+    st = np.ascontiguousarray(stakes, dtype=np.uint64)
+    peers = np.zeros(25 * asz, dtype=np.uint32)
+    lens = np.zeros(25, dtype=np.uint8)
+    rot = lib.or_replay_node_entries(seed, _ptr(st), len(st), node, asz, p, rounds, _ptr(peers), _ptr(lens), asz)
+    if rot < 0:
+        raise ValueError(lib.or_last_error().decode())
+    return peers.reshape(25, asz), lens, rot
 
 
 class Stats:

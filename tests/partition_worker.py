@@ -36,9 +36,15 @@ def main():
     rank = tdist.get_rank()
     st = stakes_of(case, eb.synth)
     pe = gp.PartitionedEngine(st, len(CASES[case]["mi"]), device=0, seed=CASES[case]["seed"],
-                              rotation_probability=CASES[case]["p"])
-    out = run_case(pe, case, st)
+                              rotation_probability=CASES[case]["p"],
+                              exchange=os.environ.get("GS_PART_EXCHANGE", "auto"))
+    modes = []
+    out = run_case(pe, case, st, ranges=[(pe.node_lo, pe.node_hi)],
+                   on_round=lambda r, e: modes.append((r, e.last_mode or "", e.records)))
     out["lo"], out["hi"] = np.array([pe.node_lo]), np.array([pe.node_hi])
+    out["xmodes"] = np.array([m for _, m, _ in modes])
+    out["xrecords"] = np.array([n for _, _, n in modes], dtype=np.uint64)
+    out["xbytes"] = np.array([pe.bytes_in], dtype=np.uint64)
     info = pe.info()
     out["bytes"] = np.array([info["device_bytes"], info["pair_bytes"], info["other_bytes"]], dtype=np.uint64)
     np.savez(os.environ["GS_PART_OUT"], **out)
@@ -47,7 +53,9 @@ def main():
         pickle.dump(rows, f)  # (this test's own output, read back by the test)
     tdist.barrier()
     tdist.destroy_process_group()
-    print(f"rank {rank}: nodes [{pe.node_lo}, {pe.node_hi}) ok", flush=True)
+    print(f"rank {rank}: nodes [{pe.node_lo}, {pe.node_hi}) device bytes {info['device_bytes']} "
+          f"(per-pair {info['pair_bytes']}, other {info['other_bytes']}); exchange received {pe.bytes_in} B; "
+          f"rounds (mode, records): {[(m, n) for _, m, n in modes if m]} ok", flush=True)
 
 
 if __name__ == "__main__":

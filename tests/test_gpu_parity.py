@@ -110,10 +110,12 @@ def test_pruning_kat_on_gpu(mode):
 
 
 # ------------------------------------------------------ Philox-mode parity ----
-def make_pair(n, origin_ranks, *, asz=12, fanout=6, p=0.013333, seed=7, thr=0.15, mi=2, mode=gs.GS_BFS_AUTO):
+def make_pair(n, origin_ranks, *, asz=12, fanout=6, p=0.013333, seed=7, thr=0.15, mi=2, mode=gs.GS_BFS_AUTO,
+              extra=None):
     pks, st = eb.synth.network(n)
     S = len(origin_ranks)
-    eng = gs.Engine(st, S, fanout=fanout, active_set_size=asz, rotation_probability=p, seed=seed, **ekw(mode))
+    eng = gs.Engine(st, S, fanout=fanout, active_set_size=asz, rotation_probability=p, seed=seed,
+                    **{**ekw(mode), **(extra or {})})
     sims = [ob.Sim(ob.PHILOX, seed, pks, st, fanout) for _ in range(S)]
     origins = [sims[0].find_nth_largest(r) for r in origin_ranks]
     eng.set_slots(origins, mi, thr)
@@ -138,8 +140,8 @@ def test_init_active_sets_parity(n, asz):
 
 
 def run_parity(n, ranks, rounds, *, p, mode, thr=0.15, mi=2, asz=12, fanout=6, fail_at=None, fractions=None,
-               full_every=5):
-    eng, sims, origins, st = make_pair(n, ranks, asz=asz, fanout=fanout, p=p, thr=thr, mi=mi, mode=mode)
+               full_every=5, extra=None):
+    eng, sims, origins, st = make_pair(n, ranks, asz=asz, fanout=fanout, p=p, thr=thr, mi=mi, mode=mode, extra=extra)
     thr_v = np.broadcast_to(np.asarray(thr, dtype=float), (len(ranks),))
     mi_v = np.broadcast_to(np.asarray(mi), (len(ranks),))
     total_prunes = 0
@@ -204,6 +206,19 @@ def test_round_by_round_parity(mode):
     """Every step of 45 rounds, 5 origins, heavy rotation: state identical to the oracle."""
     total = run_parity(240, [1, 2, 7, 60, 240], 45, p=0.08, mode=mode, full_every=4)
     assert total > 0  # the ~20-round prune waves were exercised
+
+
+@pytest.mark.parametrize("mode,extra", [
+    (gs.GS_BFS_MULTI, dict(no_small_levels=True)),      # every level through k_mv_expand / k_mv_apply
+    (gs.GS_BFS_BINNED, dict(binned_all_levels=False)),  # k_bin_small + the direct levels (the default hybrid)
+    (gs.GS_BFS_BINNED, dict(binned_all_levels=False, no_small_levels=True)),  # every level direct, grid-wide
+    (gs.GS_BFS_BINNED, dict(wide_records=True)),        # every level binned, 8-byte records
+])
+def test_round_by_round_parity_level_kernels(mode, extra):
+    """The same 45 rounds with the grid-wide level kernels (or the small-level kernels) that
+    the default small-network paths skip, each directly against the oracle."""
+    total = run_parity(240, [1, 2, 7, 60, 240], 45, p=0.08, mode=mode, full_every=4, extra=extra)
+    assert total > 0
 
 
 @pytest.mark.parametrize("mode", [gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI])

@@ -1,0 +1,158 @@
+"""Oracle parity above the sizes the reference-structure oracle can initialise itself.
+
+The oracle's initialize_gossip is O(25 N^2) (every entry shuffles all N candidates), so
+the whole-simulation parity tests stop at 3,000 nodes. Two checks pin the engine to the
+oracle at large N anyway:
+
+- Active sets at 1M and 10M nodes: the determinism contract makes a node's entries a
+  function of (seed, its id, the rounds) only, so the oracle replays ONE node's
+  initialize_gossip (gossip.rs:805-813) and chance_to_rotate (gossip.rs:739-754) -- the
+  same Philox INIT / DECIDE / ROTATE streams, PushActiveSetEntry::rotate over the
+  id-ordered candidates (push_active_set.rs:73-114, 153-187) -- and every entry of sampled
+  nodes must equal the engine's (its prefix-sum index tables at L = 17 and 20).
+- Whole rounds at 100k nodes: the oracle is handed the engine's active sets (bulk entry
+  upload) and then runs the reference's rounds itself; p = 0 keeps the sets fixed. For
+  24 rounds, through the first prune wave, every BFS/consume variant of the engine must
+  match it in hops, inbound (src, hop) lists, prunes, counters, prune state and received
+  caches (node ids above 65,535; 4-byte and 8-byte binned records; the grid-wide and the
+  single-workgroup level kernels).
+
+Node pubkeys are stand-ins 0xA5 || 0^23 || id (big-endian): all encode to 44 base58
+characters, so base58 order -- the reference's consume tie-break (gossip.rs:639-645) and
+the node-id rule of the determinism contract -- is id order.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import engine_bind as eb
+import oracle_bind as ob
+from test_oracle_replay import stand_in_pubkeys
+
+gs = eb.gs
+pytestmark = pytest.mark.gpu
+U64MAX = np.uint64(2**64 - 1)
+
+
+def engine_entries(eng, node):
+    out = np.full((25, eng.active_set_size), 0xFFFFFFFF, dtype=np.uint32)
+    lens = np.zeros(25, dtype=np.uint8)
+    for k in range(25):
+        e = eng.get_entry(node, k)
+        lens[k] = len(e)
+        out[k, :len(e)] = e
+    return out, lens
+
+
+def check_replay(eng, st, seed, nodes, p, rounds):
+    """Every entry of `nodes` equals the oracle's one-node replay; returns rotations per node."""
+    asz = eng.active_set_size
+    with ThreadPoolExecutor(max_workers=8) as ex:  # (the C replay releases the GIL)
+        reps = list(ex.map(lambda v: ob.replay_node_entries(seed, st, v, asz, p, rounds), nodes))
+    rot = {}
+    for v, (peers, lens, nrot) in zip(nodes, reps):
+        gp, gl = engine_entries(eng, v)
+        np.testing.assert_array_equal(gl, lens, err_msg=f"entry lengths of node {v} after {rounds} rounds")
+        np.testing.assert_array_equal(gp, peers, err_msg=f"entries of node {v} after {rounds} rounds")
+        rot[v] = nrot
+    return rot
+
+
+@pytest.mark.parametrize("n,n_sample", [(1_000_000, 16), (10_000_000, 4)])
+def test_active_sets_match_oracle_replay_at_scale(n, n_sample):
+    """initialize_gossip and 20 rounds of chance_to_rotate at 1M / 10M nodes, sampled nodes'
+    every entry (16 x 25 / 4 x 25 entries) against the oracle's replay of that node."""
+    seed, p, rounds = 0x5EED0003, 0.05, 20
+    st = eb.synth.power_law_stakes(n)
+    rng = np.random.default_rng(n)
+    eng = gs.Engine(st, 1, rotation_probability=p, seed=seed)
+    eng.set_slots([0])
+    eng.init_active_sets()
+    fixed = [0, 1, n // 2, n - 1]  # the two largest stakes (top buckets), the middle, the smallest
+    init_nodes = sorted(set(fixed[:max(2, n_sample // 4)] + rng.choice(n, n_sample, replace=False).tolist()))
+    check_replay(eng, st, seed, init_nodes, p, 0)
+    for r in range(rounds):
+        eng.chance_to_rotate(r)
+    # nodes that rotated at least once (P = 1 - 0.95^20 = 0.64) and some that did not
+    rot_nodes = sorted(set(init_nodes[:2] + rng.choice(n, 2 * n_sample, replace=False).tolist()))
+    rot = check_replay(eng, st, seed, rot_nodes, p, rounds)
+    assert sum(1 for x in rot.values() if x > 0) >= n_sample // 2, rot
+    eng.close()
+
+
+# ------------------------------------------------------- 100k: whole rounds ----
+VARIANTS = {  # name: engine kwargs (one origin slot each; results must be identical)
+    "binned": dict(bfs_mode=gs.GS_BFS_BINNED),  # default hybrid: single-workgroup small levels, direct levels
+    "binned_grid_direct": dict(bfs_mode=gs.GS_BFS_BINNED, no_small_levels=True),
+    "binned_all": dict(bfs_mode=gs.GS_BFS_BINNED, binned_all_levels=True),  # 4-byte records
+    "binned_all_wide": dict(bfs_mode=gs.GS_BFS_BINNED, binned_all_levels=True, wide_records=True),
+    "multi": dict(bfs_mode=gs.GS_BFS_MULTI),
+    "multi_no_small": dict(bfs_mode=gs.GS_BFS_MULTI, no_small_levels=True),
+    "level": dict(bfs_mode=gs.GS_BFS_LEVEL),
+}
+
+
+def test_rounds_match_oracle_with_engine_active_sets_100k():
+    n, seed, rounds, thr, mi = 100_000, 0x5EED0007, 24, 0.15, 2
+    st = eb.synth.power_law_stakes(n)
+    origin = int(np.lexsort((np.arange(n), -st.astype(np.float64)))[0])  # origin rank 1
+    engs = {}
+    for name, kw in VARIANTS.items():
+        e = gs.Engine(st, 1, rotation_probability=0.0, seed=seed, **kw)
+        e.set_slots([origin], mi, thr)
+        e.init_active_sets()
+        engs[name] = e
+    peers, lens = engs["binned"].active_sets()
+    for name, e in engs.items():
+        if name != "binned":
+            p2, l2 = e.active_sets()
+            assert np.array_equal(p2, peers) and np.array_equal(l2, lens), name
+    sim = ob.Sim(ob.PHILOX, seed, stand_in_pubkeys(n), st, 6)
+    sim.set_entries(peers, lens)
+    del peers, lens
+    pruned_total = 0
+    for r in range(rounds):
+        sim.run_gossip(origin)
+        want_d = sim.distances()
+        w_off, w_src, w_hop = sim.orders_all(64 * n)
+        for name, e in engs.items():
+            e.run_gossip()
+            np.testing.assert_array_equal(e.distances(0), want_d, err_msg=f"{name} hops round {r}")
+            off, src, hop = e.inbound(0, cap=len(w_src) + 1)
+            np.testing.assert_array_equal(off, w_off, err_msg=f"{name} in-degrees round {r}")
+            np.testing.assert_array_equal(src[:len(w_src)], w_src, err_msg=f"{name} inbound sources round {r}")
+            np.testing.assert_array_equal(hop[:len(w_hop)], w_hop, err_msg=f"{name} inbound hops round {r}")
+        sim.consume_messages(origin)
+        sim.send_prunes(origin, thr, mi)
+        want_p = sim.prunes()
+        pruned_total += len(want_p)
+        full = r % 6 == 0 or 18 <= r <= 21 or r == rounds - 1
+        if full:
+            oup, oln, okeys, osc = sim.caches(origin)
+            has = oup != 0xFFFFFFFF
+        for name, e in engs.items():
+            e.consume_messages()
+            e.send_prunes()
+            assert e.prunes(0) == want_p, f"{name} prunes round {r}"
+            if full:
+                up, ln, keys, sc = e.caches(0)
+                np.testing.assert_array_equal(up[has], oup[has], err_msg=f"{name} upserts round {r}")
+                np.testing.assert_array_equal(up[~has], 0)
+                np.testing.assert_array_equal(ln, oln, err_msg=f"{name} cache lengths round {r}")
+                np.testing.assert_array_equal(keys, okeys, err_msg=f"{name} cache keys round {r}")
+                np.testing.assert_array_equal(sc, osc, err_msg=f"{name} cache scores round {r}")
+        sim.prune_connections()
+        oe, oi, op = sim.counters()
+        om = sim.pruned_all(origin)
+        for name, e in engs.items():
+            e.prune_connections()
+            eg, ig, pr = e.counters(0)
+            np.testing.assert_array_equal(eg, np.where(oe == U64MAX, 0, oe), err_msg=f"{name} egress round {r}")
+            np.testing.assert_array_equal(ig, np.where(oi == U64MAX, 0, oi), err_msg=f"{name} ingress round {r}")
+            np.testing.assert_array_equal(pr, op, err_msg=f"{name} prune-sent round {r}")
+            np.testing.assert_array_equal(e.pruned_all(0), om, err_msg=f"{name} prune state round {r}")
+    assert pruned_total > 0  # the first prune wave happened inside the window
+    assert int(w_src.max()) >= 65536  # ids beyond u16
+    for e in engs.values():
+        e.close()

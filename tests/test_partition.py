@@ -31,13 +31,13 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(tmp_path, case, backend, world=2):
+def run_ranks(tmp_path, case, backend, world=2, exchange="auto", extra_env=None):
     port = free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), GS_PART_OUT=str(tmp_path / f"rank{r}.npz"), GS_PART_CASE=case,
-                   GS_PART_BACKEND=backend)
+                   GS_PART_BACKEND=backend, GS_PART_EXCHANGE=exchange, **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "partition_worker.py")], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     try:
@@ -52,6 +52,7 @@ def run_ranks(tmp_path, case, backend, world=2):
         pytest.skip("RCCL refused two ranks on the box's one GPU: " + " | ".join(l.strip()[-300:] for l in logs))
     for p, log in zip(procs, logs):
         assert p.returncode == 0, log[-3000:]
+        print(log.strip()[-2000:])
     parts = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
     caches = []
     for r in range(world):
@@ -60,10 +61,27 @@ def run_ranks(tmp_path, case, backend, world=2):
     return parts, caches
 
 
+def test_partition_ranges_refuse_empty_ranks():
+    import gossip_sim_amd.partition as gp
+    assert gp.partition_ranges(3000, 2) == [(0, 2048), (2048, 3000)]
+    assert gp.partition_ranges(10_000_000, 8)[-1][1] == 10_000_000
+    with pytest.raises(ValueError, match="without nodes"):
+        gp.partition_ranges(3000, 4)  # ranges of 1,024: the fourth rank would start at 3,072
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("case,backend", [("small", "gloo"), ("small", "nccl"), ("large", "gloo")])
-def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend):
-    parts, caches = run_ranks(tmp_path, case, backend)
+@pytest.mark.parametrize("case,backend,exchange", [
+    ("small", "gloo", "auto"), ("small", "gloo", "dense"), ("small", "nccl", "auto"),
+    ("large", "gloo", "auto"), ("large", "gloo", "records")])
+def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend, exchange):
+    """(exchange: auto = records outside prune waves, dense in them; records / dense forced.)"""
+    extra = {"GS_PART_RECORD_CAP": str(1 << 25)} if exchange == "records" else None
+    parts, caches = run_ranks(tmp_path, case, backend, exchange=exchange, extra_env=extra)
+    modes = set(str(m) for m in parts[0]["xmodes"] if str(m))
+    if exchange != "auto":
+        assert modes == {exchange}, modes
+    elif case == "large":
+        assert "dense" in modes, modes  # the prune wave outgrows the record buffer
     c = CASES[case]
     st = stakes_of(case, eb.synth)
     S = len(c["mi"])
@@ -97,3 +115,39 @@ def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend):
             assert abs(pair - share * fi["pair_bytes"]) <= 0.01 * fi["pair_bytes"] + (64 << 20), (pair, fi)
             assert abs(other - fi["other_bytes"]) <= 0.02 * fi["other_bytes"], (other, fi)
             assert dev < 0.8 * fi["device_bytes"], (dev, fi)
+
+
+@pytest.mark.gpu
+def test_partition_c5_as_configured(tmp_path):
+    """BASELINE C5 as configured on the box's one GPU: 10M nodes, origin ranks 1..16 as 16
+    slots, node-range partitioned over two gloo ranks (two engines on device 0), 22 rounds
+    through the first prune wave (records exchanged in ordinary rounds, dense words in the
+    wave). Equals one unpartitioned engine (the level-synchronous BFS) bit for bit: every
+    per-round summary and hop histogram, per-rank digests of owned hops and accumulators,
+    the replicated prune state, sampled caches; and the size-independent BFS properties
+    hold on the unpartitioned run."""
+    from test_gpu_parity import _invariants
+    parts, caches = run_ranks(tmp_path, "c5", "gloo")
+    c = CASES["c5"]
+    n, S = c["n"], len(c["mi"])
+    ranges = [(int(p["lo"][0]), int(p["hi"][0])) for p in parts]
+    assert ranges[0][0] == 0 and ranges[0][1] == ranges[1][0] and ranges[1][1] == n
+    modes = [str(m) for m in parts[0]["xmodes"]]
+    assert "dense" in modes and "records" in modes, modes  # the prune wave went dense
+    st = stakes_of("c5", eb.synth)
+    one = eb.gs.Engine(st, S, bfs_mode=eb.gs.GS_BFS_LEVEL, seed=c["seed"], rotation_probability=c["p"])
+    want = run_case(one, "c5", st, ranges=ranges)
+    want_caches = {k: cache_rows(one, "c5", k) for k in range(S)}
+    summ = want["summaries"]
+    assert summ["prunes"].sum() > 0 and (summ["visited"] > 0.9 * n).all()
+    for k in (0, S - 1):
+        _invariants(one, k, n, summ[-1, k])
+    one.close()
+    for r, p in enumerate(parts):
+        np.testing.assert_array_equal(p["summaries"], summ)
+        for k in range(S):
+            np.testing.assert_array_equal(p[f"hist{k}"], want[f"hist{k}"])
+            assert p[f"pruned{k}"][0] == want[f"pruned{k}"][0], f"prune state slot {k}"
+            assert list(p[f"dig{k}"][0]) == list(want[f"dig{k}"][r]), f"rank {r} slot {k}"
+            for v, row in caches[r][k].items():
+                assert row == want_caches[k][v], f"cache slot {k} node {v}"
