@@ -14,13 +14,14 @@ waves, where pushes per origin-round settle near 3N).
 value = pushes to non-failed peers over all slots and ranks / wall time of the K
 timed steps (max over ranks).
 
-Multi-GPU (one process per GPU): by default every rank runs its own 3,000-origin
-network (seed + rank, "scaling": "weak"). With --shard-origins the ranks split the
-SAME 3,000 origins of ONE network (rank r takes origins [r*S/K, (r+1)*S/K)), the
-run is "strong" scaling, and rank 0 checks the gathered per-round summaries of
-every origin against the same origins run on one engine when --check-shard is set.
-torch.distributed carries only the barrier, the timing max/sum and the summary
-gather.
+Multi-GPU (one process per GPU): the ranks split the 3,000 origins of ONE network
+(same seed, so the same active-set trajectory; rank r takes origins [r*S/K,
+(r+1)*S/K)): "strong" scaling, and with --check-shard rank 0 checks the gathered
+per-round summaries of every origin against all origins run on one engine.
+--per-rank-networks gives every rank its own 3,000-origin network instead (seed +
+rank, "weak"). --workload c4 deals BASELINE C4's 13 sweep sims (1M nodes) over the
+ranks instead (sweep sharding). torch.distributed carries only the barrier, the
+timing max/sum and the summary gather.
 
 roofline: the dominant kernel (k_round_wg) with SURVEY.md 8(d) algorithmic bytes
 per launch, divided by that kernel's average duration measured with hipEvents on
@@ -202,15 +203,15 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
                                      "B_prop (SURVEY 8d), summed over slots", f"bfs_{mode}_c4")}
 
 
-def c5_leg(gs, synth, args, nodes=10_000_000, slots=2, warmup=3, steps=10):
-    """BASELINE C5's graph on one GPU: a 10M-node network, origin ranks 1 and 2 as slots of
-    ONE engine (multi-source BFS). A node-range partition over K ranks divides the per-pair
-    state, but every rank runs this whole BFS, so this is the per-GPU
-    propagation work of C5."""
+def c5_leg(gs, synth, args, nodes=10_000_000, slots=16, warmup=3, steps=10):
+    """BASELINE C5 as configured, on one GPU: a 10M-node network, origin ranks 1..16 as 16
+    slots of ONE engine (the multi-source BFS over one slot group). A node-range partition
+    over K ranks divides the per-(slot, node) state; every rank runs this whole BFS
+    (DESIGN.md section 7), so the propagation figures are the per-GPU work of C5."""
     import numpy as np
     stakes = synth.power_law_stakes(nodes)
-    order = np.argsort(-stakes.astype(np.float64), kind="stable")
-    origins = [int(order[0]), int(order[1])][:slots]
+    order = np.lexsort((np.arange(nodes), -stakes.astype(np.float64)))  # rank order, ties by id
+    origins = [int(x) for x in order[:slots]]
     eng = gs.Engine(stakes, len(origins), fanout=args.fanout, active_set_size=args.active_set_size,
                     rotation_probability=0.013333, seed=args.seed, device=0, profile=True, bfs_mode=args.large_mode)
     eng.set_slots(origins, args.min_ingress, args.threshold)
@@ -234,14 +235,16 @@ def c5_leg(gs, synth, args, nodes=10_000_000, slots=2, warmup=3, steps=10):
     info = eng.info()
     eng.close()
     mode = {2: "level", 3: "binned", 4: "multi"}.get(info["bfs_mode"], str(info["bfs_mode"]))
-    return {"workload": f"C5 graph on one GPU: {nodes}-node power-law network, origin ranks 1-{len(origins)} as "
+    return {"workload": f"C5 on one GPU: {nodes}-node power-law network, origin ranks 1-{len(origins)} as "
                         f"slots of one engine (unpartitioned; every partition rank runs this BFS)",
             "bfs_mode": mode, "rounds": [warmup, warmup + steps], "ms_per_step": dt / steps * 1e3,
-            "edges_per_s": E / dt, "init_active_sets_s": t_init,
+            "edges_per_s": E / dt, "origin_rounds_per_s": len(origins) * steps / dt,
+            "pushes_per_origin_round": E / (len(origins) * steps), "init_active_sets_s": t_init,
             "us_per_round": {k: round(v * 1e3 / steps, 1) for k, v in fam.items()},
-            "device_bytes": info["device_bytes"],
+            "device_bytes": info["device_bytes"], "pair_bytes": info["pair_bytes"],
             "bfs_roofline": roofline(b_prop(V, E, args.active_set_size), fam["bfs"] + fam["gather"], steps,
-                                     f"BFS ({mode})", "B_prop (SURVEY 8d), summed over slots")}
+                                     f"BFS ({mode}" + (": expand/apply per level + gather)" if mode == "multi" else ")"),
+                                     "B_prop (SURVEY 8d), summed over slots", f"bfs_{mode}_c5")}
 
 
 def c3_leg(gs, synth, args, nodes=100_000, warmup=5, steps=20):
@@ -290,7 +293,62 @@ def c3_leg(gs, synth, args, nodes=100_000, warmup=5, steps=20):
     return {"workload": f"C3 per-GPU share: {nodes}-node network, active-set-size sweep values 12 and 20, one "
                         f"engine (stream, host thread) each, run concurrently, origin rank 1", "bfs_mode": mode, "rounds": [warmup, warmup + steps],
             "ms_per_step": dt / steps * 1e3, "edges_per_s": E / dt,
-            "bfs_roofline": roofline(bp, b_ms, 2 * steps, f"BFS ({mode})", "B_prop (SURVEY 8d)")}
+            "bfs_roofline": roofline(bp, b_ms, 2 * steps, f"BFS ({mode})", "B_prop (SURVEY 8d)", f"bfs_{mode}_c3")}
+
+
+def c4_sweep_sharded(gs, synth, args, rank, world, dev, barrier, reduce, nodes=1_000_000):
+    """--workload c4: BASELINE C4's sweep sims (fail-nodes 0.1..0.5 at when-to-fail 0, then
+    prune-stake-threshold 0.05..0.40) dealt round-robin over the ranks (sweep.shard); each
+    rank runs its sims as slots of one engine over the SAME 1M-node network and seed. The
+    total work is fixed (strong scaling); value = all ranks' pushes / the slowest rank's time."""
+    import numpy as np
+    shard = list(range(rank, 13, world))
+    stakes = synth.power_law_stakes(nodes)
+    origin = int(np.argmax(stakes))
+    fr_all = [0.1, 0.2, 0.3, 0.4, 0.5] + [0.0] * 8
+    thr_all = [args.threshold] * 5 + [round(0.05 * (j + 1), 2) for j in range(8)]
+    E = 0.0
+    eng = None
+    if shard:
+        eng = gs.Engine(stakes, len(shard), fanout=args.fanout, active_set_size=args.active_set_size,
+                        rotation_probability=0.013333, seed=args.seed, device=dev, profile=True,
+                        bfs_mode=args.large_mode)
+        eng.set_slots([origin] * len(shard), args.min_ingress, [thr_all[i] for i in shard])
+        eng.init_active_sets()
+        eng.fail_nodes([fr_all[i] for i in shard])  # when-to-fail 0 (gossip_main.rs:449-452)
+        for r in range(args.warmup):
+            eng.round(r, record=False)
+        eng.sync()
+        eng.kernel_time_reset()
+    barrier()
+    t0 = time.perf_counter()
+    if eng:
+        for r in range(args.warmup, args.warmup + args.steps):
+            eng.round(r, record=True)
+        eng.sync()
+    barrier()
+    dt = reduce(time.perf_counter() - t0, lambda d: d.ReduceOp.MAX)
+    roof = None
+    if eng:
+        summ = eng.summaries()
+        E = float(summ["pushes"].astype("float64").sum())
+        V = float(summ["visited"].astype("float64").sum())
+        fam = sum(eng.kernel_time(k)[0] for k in ("bfs", "gather", "gather_consume"))
+        roof = roofline(b_prop(V, E, args.active_set_size), fam, args.steps, "BFS (this rank's slot group)",
+                        "B_prop (SURVEY 8d), summed over the rank's slots")
+        mode = eng.info()["bfs_mode"]
+        eng.close()
+    E_all = reduce(E, lambda d: d.ReduceOp.SUM)
+    return {"metric": METRIC, "value": E_all / dt, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (deterministic Philox power-law stakes, SURVEY.md 8(d))",
+            "config": {"workload": f"C4: {nodes}-node power-law network, origin rank 1, fail-nodes 0.1..0.5 + "
+                                   "prune-stake-threshold 0.05..0.40 (13 sims) dealt round-robin over the ranks",
+                       "nodes": nodes, "sims_total": 13, "sims_rank0": len(shard), "rounds":
+                       [args.warmup, args.warmup + args.steps], "parallelism": f"sweep-sharded x{world} (one network)",
+                       "bfs_mode": mode if shard else None},
+            "origin_rounds_per_s": 13 * args.steps / dt, "roofline_rank0": roof, "cpu_baseline": None}
 
 
 # ------------------------------------------------------------------------ main ----
@@ -318,10 +376,16 @@ def main():
     ap.add_argument("--only-large", action="store_true", help="run only the c4 / c3 legs (A/B of BFS modes)")
     ap.add_argument("--legs", default="c4,c3", help="with --only-large: which legs (e.g. c4 for a PMC pass)")
     ap.add_argument("--shard-origins", action="store_true",
-                    help="ranks split the origins of ONE network (strong scaling) instead of one network each")
+                    help="ranks split the origins of ONE network (strong scaling; the default with WORLD_SIZE > 1)")
+    ap.add_argument("--per-rank-networks", action="store_true",
+                    help="with WORLD_SIZE > 1: every rank runs all origins of its own network (seed + rank, weak)")
     ap.add_argument("--check-shard", action="store_true",
-                    help="with --shard-origins: rank 0 re-runs all origins on one engine and compares")
+                    help="with origin sharding: rank 0 re-runs all origins on one engine and compares")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4"],
+                    help="c4: BASELINE C4's 13 sims (1M nodes) dealt round-robin over the ranks (sweep sharding)")
     args = ap.parse_args()
+    if not args.per_rank_networks:
+        args.shard_origins = True  # one network, its origins split over the ranks (all of them at N = 1)
 
     gs = load_pkg()          # loads libgossip_hip.so (and its HIP runtime) before torch, if torch is used at all
     gs.lib()
@@ -355,6 +419,14 @@ def main():
         t = dist[0].tensor([x], dtype=dist[0].float64)
         dist[1].all_reduce(t, op=op(dist[1]))
         return float(t.item())
+
+    if args.workload == "c4":
+        out = c4_sweep_sharded(gs, synth, args, rank, world, dev, barrier, reduce)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist:
+            dist[1].destroy_process_group()
+        return
 
     pks, stakes = synth.network(args.nodes)
     S_all = args.slots or args.nodes
@@ -461,7 +533,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if args.shard_origins else "weak",
+        "scaling": "weak" if args.per_rank_networks else "strong",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (deterministic Philox power-law stakes, SURVEY.md 8(d))",

@@ -160,9 +160,12 @@ static size_t part_record_cap(size_t N, size_t S, uint32_t K) {
   return std::max<size_t>(1u << 16, (S * N) / (2 * (size_t)K));
 }
 
-// K == 1: an engine over all nodes; K > 1: rank `rank` of a node-range partition.
+// K == 0: an engine over all nodes; K >= 1: rank `rank` of a node-range partition over K
+// ranks (K == 1: one rank owning every node, the exchange calls still available).
 static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t n_slots, uint32_t rank,
                          uint32_t K, gs_engine** out) {
+  const bool part = K >= 1;
+  if (!part) K = 1;
   if (!prm || !stakes || !out) return fail(GS_EINVAL, "null argument");
   *out = nullptr;
   if (n < 2 || n > GS_MAX_NODES) return fail(GS_EINVAL, "n_nodes must be in [2, 2^24-1]");
@@ -206,7 +209,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   const bool bin_ok = pairs <= (1ull << 28) && bin_supported(e->bin, e->fcap);
   mv_geometry(n, n_slots, e->ASZ, e->ASZP, e->mv);
   const bool mv_ok = mv_supported(e->mv, e->ASZP);
-  if (K > 1) {  // a partition rank runs the multi-source BFS over its replicated tables
+  if (part) {  // a partition rank runs the multi-source BFS over its replicated tables
     if (mode != GS_BFS_AUTO && mode != GS_BFS_MULTI) {
       destroy_engine(e);
       return fail(GS_EINVAL, "a node-range partition runs bfs_mode GS_BFS_MULTI (or AUTO)");
@@ -422,7 +425,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
 }
 
 int gs_create(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t n_slots, gs_engine** out) {
-  return create_engine(prm, stakes, n, n_slots, 0, 1, out);
+  return create_engine(prm, stakes, n, n_slots, 0, 0, out);
 }
 
 int gs_create_part(const gs_params* prm, const uint64_t* stakes, uint32_t n, uint32_t n_slots, uint32_t rank,

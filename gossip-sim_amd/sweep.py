@@ -104,7 +104,7 @@ def allreduce_results(local, n_sims, *, group=None, device=None):
     for i, arrs in local.items():
         for j, key in enumerate(NAMES):
             lens[i, j] = len(arrs[key])
-    if world > 1:
+    if tdist is not None:  # (a one-rank group still runs the collective: RCCL is exercised)
         import torch
         t = torch.from_numpy(lens).to(device) if device is not None else torch.from_numpy(lens)
         tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=group)
@@ -116,7 +116,7 @@ def allreduce_results(local, n_sims, *, group=None, device=None):
         for j, (kind, name) in enumerate(NAMES):
             k = i * nn + j
             buf[offs[k]:offs[k + 1]] = _as_bits(kind, arrs[(kind, name)])
-    if world > 1:
+    if tdist is not None:  # (a one-rank group still runs the collective: RCCL is exercised)
         import torch
         t = torch.from_numpy(buf).to(device) if device is not None else torch.from_numpy(buf)
         tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=group)

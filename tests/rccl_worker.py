@@ -1,0 +1,58 @@
+"""One process, one rank (tests/test_rccl.py): every torch.distributed exchange of the
+engine's multi-GPU paths over the backend GS_RCCL_BACKEND (nccl = RCCL on ROCm, or gloo),
+world size 1 on cuda:0. Writes the results to GS_RCCL_OUT (npz):
+  part_<exchange>_*  the node-range partition's small case (PartitionedEngine: prune
+                     records / dense words and statistics through device buffers)
+  sweep_*            a sharded fail-nodes sweep (sweep.run_sharded -> allreduce_results)
+  rows               sweep.gather_rows of a byte matrix (the origin-shard reassembly)"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import engine_bind as eb  # noqa: E402
+
+from partition_case import CASES, run_case, stakes_of  # noqa: E402
+
+
+def main():
+    import torch
+    import torch.distributed as tdist
+    import gossip_sim_amd.partition as gp
+    import gossip_sim_amd.sweep as sw
+    backend = os.environ["GS_RCCL_BACKEND"]
+    tdist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{os.environ['GS_RCCL_PORT']}", rank=0,
+                             world_size=1)
+    torch.cuda.set_device(0)
+    out = {}
+    st = stakes_of("small", eb.synth)
+    c = CASES["small"]
+    for exchange in ("records", "dense"):
+        pe = gp.PartitionedEngine(st, len(c["mi"]), device=0, seed=c["seed"], rotation_probability=c["p"],
+                                  exchange=exchange)
+        modes = []
+        res = run_case(pe, "small", st, on_round=lambda r, e: modes.append(e.last_mode or ""))
+        assert pe.on_device == (backend == "nccl")
+        for k, v in res.items():
+            out[f"part_{exchange}_{k}"] = v
+        out[f"part_{exchange}_modes"] = np.array(modes)
+        pe.close()
+    _, st90 = eb.synth.network(90)
+    res = sw.run_sharded(st90, n_sims=3, origin_ranks=[1, 2, 1], fractions=[0.1, 0.0, 0.3], device=0,
+                         comm_device="cuda:0" if backend == "nccl" else None, fanout=6, asz=12, iterations=24,
+                         warm_up=4, p=0.05, thr=0.15, min_ingress_nodes=2, fraction_to_fail=0.1, when_to_fail=3,
+                         test_type=5, seed=7)
+    for i in range(3):
+        for kind, name in sw.NAMES:
+            out[f"sweep_{kind}:{name}:{i}"] = res.f64(i, name) if kind == "f" else res.u64(i, name)
+    rows = np.arange(5 * 6 * 8, dtype=np.uint8).reshape(5, 48)
+    out["rows"] = sw.gather_rows((torch, tdist), rows, 6, 1, row_bytes=8)
+    out["backend"] = np.array([tdist.get_backend()])
+    np.savez(os.environ["GS_RCCL_OUT"], **out)
+    tdist.destroy_process_group()
+    print(f"{backend}: ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -111,8 +111,10 @@ def test_pruning_kat_on_gpu(mode):
 
 # ------------------------------------------------------ Philox-mode parity ----
 def make_pair(n, origin_ranks, *, asz=12, fanout=6, p=0.013333, seed=7, thr=0.15, mi=2, mode=gs.GS_BFS_AUTO,
-              extra=None):
+              extra=None, stakes=None):
     pks, st = eb.synth.network(n)
+    if stakes is not None:
+        st = np.ascontiguousarray(stakes, dtype=np.uint64)
     S = len(origin_ranks)
     eng = gs.Engine(st, S, fanout=fanout, active_set_size=asz, rotation_probability=p, seed=seed,
                     **{**ekw(mode), **(extra or {})})
@@ -140,8 +142,9 @@ def test_init_active_sets_parity(n, asz):
 
 
 def run_parity(n, ranks, rounds, *, p, mode, thr=0.15, mi=2, asz=12, fanout=6, fail_at=None, fractions=None,
-               full_every=5, extra=None):
-    eng, sims, origins, st = make_pair(n, ranks, asz=asz, fanout=fanout, p=p, thr=thr, mi=mi, mode=mode, extra=extra)
+               full_every=5, extra=None, stakes=None):
+    eng, sims, origins, st = make_pair(n, ranks, asz=asz, fanout=fanout, p=p, thr=thr, mi=mi, mode=mode, extra=extra,
+                                       stakes=stakes)
     thr_v = np.broadcast_to(np.asarray(thr, dtype=float), (len(ranks),))
     mi_v = np.broadcast_to(np.asarray(mi), (len(ranks),))
     total_prunes = 0
@@ -219,6 +222,26 @@ def test_round_by_round_parity_level_kernels(mode, extra):
     the default small-network paths skip, each directly against the oracle."""
     total = run_parity(240, [1, 2, 7, 60, 240], 45, p=0.08, mode=mode, full_every=4, extra=extra)
     assert total > 0
+
+
+@pytest.mark.parametrize("mode", [gs.GS_BFS_BINNED, gs.GS_BFS_MULTI])
+def test_parity_hub_in_degrees_above_64(mode):
+    """Fanout = active-set size 32 on 500 nodes whose stakes halve every 8 ranks (buckets
+    24 down to 0), inbound capacity 256: the top-stake nodes sit in most high-bucket
+    entries and receive 65-83 pushes a round -- the binned gather's whole-wave rows for
+    pairs above G_HEAVY = 64 records, the consume's single-lane path above 64 -- every
+    level binned; against the oracle round by round. (The binned gather's fallback for a
+    step with more than half its pairs heavy cannot occur: that needs a mean in-degree
+    above 32 >= fanout.)"""
+    n = 500
+    st = np.maximum(2.0 ** (54 - np.arange(n) / 8.0), 1e9).astype(np.uint64)
+    extra = dict(inbound_capacity=256, binned_all_levels=mode == gs.GS_BFS_BINNED)
+    eng, sims, origins, _ = make_pair(n, [1], asz=32, fanout=32, p=0.05, mode=mode, extra=extra, stakes=st)
+    eng.run_gossip()
+    _, ing, _ = eng.counters(0)
+    assert int((ing > 64).sum()) >= 5, int(ing.max())
+    eng.close()
+    run_parity(n, [1, 2, 40], 22, p=0.05, mode=mode, asz=32, fanout=32, full_every=7, extra=extra, stakes=st)
 
 
 @pytest.mark.parametrize("mode", [gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI])

@@ -104,8 +104,9 @@ def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend, exchang
                 np.testing.assert_array_equal(p[f"cache{k}"][lo:hi], want[f"cache{k}"][lo:hi], err_msg=f"cache {k}")
             for v, row in caches[r][k].items():
                 assert row == want_caches[k][v], f"cache slot {k} node {v}"
-    if case == "large":
+    if case == "large" and exchange == "auto":
         # device memory per rank: its share of the per-(slot, node) state + the replicated tables
+        # (the forced-records run enlarges the record buffer by GS_PART_RECORD_CAP: not compared)
         full = eb.gs.Engine(st, S, bfs_mode=eb.gs.GS_BFS_MULTI, seed=c["seed"], rotation_probability=c["p"])
         fi = full.info()
         full.close()
