@@ -180,7 +180,9 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
             del fam[k]
     phases = None
     if os.environ.get("GS_PHASE_PROFILE") == "1":  # multi gather: workgroup-ms per phase (thread 0 of each workgroup)
-        names = {12: "count", 13: "scan_place", 14: "body_light", 15: "body_all"}
+        names = {12: "count", 13: "scan_place", 14: "body_light", 15: "body_all",
+                 0: "small_setup", 1: "small_expand_loads", 2: "small_atomics_places", 3: "small_lt_barrier",
+                 4: "small_levels_e-5"}
         phases = {nm: round(eng.kernel_time("phase." + chr(65 + i))[0], 2) for i, nm in names.items()}
     info = eng.info()
     eng.close()

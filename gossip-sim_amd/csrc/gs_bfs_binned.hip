@@ -26,7 +26,11 @@
 //
 // Results equal k_bfs_level's: hops, in-degrees, the inbound record SET of each pair
 // (consume sorts them by (hop, src), gossip.rs:639-645), egress, frontier sizes.
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
+#include <vector>
 #include "gs_device.h"
 #include "gs_internal.h"
 
@@ -60,7 +64,9 @@ struct BinArgs {
   uint2* Lt;       // [256][nbins] (pool start, count) of bin b's run at level d
   uint32_t* binoff;  // [nbins] records in bin b's pool region so far this round (only bin b's apply touches it)
   uint32_t* visbm;  // [PAIRS / 32] visited pairs (hop != unreached) of this round
-  uint32_t* hlvl;   // host-mapped [256]: expand(d) writes level d's frontier size
+  uint32_t* hlvl;   // host-mapped [256]: expand(d) writes level d's frontier size (the polled loop)
+  uint32_t* dpair;  // [258] level of expand/apply pair i (predicted loop): head writes [0], pair i [i + 1]
+  uint32_t* hprof;  // host-mapped: the tail kernel's level profile (seq, levels, sizes)
   uint32_t N, ASZ, fanout, fc, capin, Gmax, PW, BS, nbins, ORW, csr_cap, qmin;
   size_t PAIRS, pool_bin_cap;  // pool region of a bin: 2^BS * capin records (in-degrees are <= capin)
   int record;
@@ -215,16 +221,25 @@ __device__ inline void bin_direct(const BinArgs& a, uint32_t d, uint32_t qn, con
 // level d0; stops at the first level with no pairs, more than BIN_SMALL, or at qmin;
 // writes (level, pairs) to the host-mapped hstate.
 constexpr uint32_t BIN_SMALL = 1024, BIN_ST = 1024;
+constexpr uint32_t BIN_NOPAIR = 0xFFFFFFFFu;
+enum : uint32_t { BIN_POLL = 0, BIN_HEAD = 1, BIN_TAIL = 2 };
+// Modes: BIN_POLL from level d0 while levels have at most lim pairs (the polled loop);
+// BIN_HEAD the same from level 0, leaving the level where it stopped in dpair[0] for the
+// expand/apply pairs of the predicted loop; BIN_TAIL from level dpair[pi] to the end of
+// the BFS whatever the sizes (correct for any level, fast for the small tail), publishing
+// the round's level profile (hprof) for the host's next prediction.
 template <int ASZP>
-__global__ __launch_bounds__(BIN_ST) void k_bin_small(BinArgs a, uint32_t d0, uint32_t lim, uint32_t* __restrict__ q0,
-                                                     uint32_t* __restrict__ q1, uint32_t* __restrict__ hstate) {
+__global__ __launch_bounds__(BIN_ST) void k_bin_small(BinArgs a, uint32_t mode, uint32_t d0, uint32_t pi, uint32_t lim,
+                                                     uint32_t* __restrict__ q0, uint32_t* __restrict__ q1,
+                                                     uint32_t* __restrict__ hstate, uint32_t seq) {
   __shared__ uint32_t s_qn;
-  uint32_t d = d0;
-  if (threadIdx.x == 0) s_qn = a.lvl[d0];
+  uint32_t d = mode == BIN_TAIL ? a.dpair[pi] : d0;
+  if (mode == BIN_TAIL) lim = 0xFFFFFFFFu;
+  if (threadIdx.x == 0) s_qn = d < 256 ? a.lvl[d] : 0u;
   __syncthreads();
   uint32_t qn = s_qn;
   while (qn > 0 && qn <= lim && d < 254) {
-    if (threadIdx.x == 0) __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0 && mode == BIN_POLL) __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     bin_direct<ASZP>(a, d, qn, (d & 1) ? q1 : q0, (d & 1) ? q0 : q1);
     __syncthreads();
     if (threadIdx.x == 0) s_qn = __hip_atomic_load(&a.lvl[d + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -233,20 +248,38 @@ __global__ __launch_bounds__(BIN_ST) void k_bin_small(BinArgs a, uint32_t d0, ui
     ++d;
   }
   if (threadIdx.x == 0) {
+    if (mode == BIN_HEAD) a.dpair[0] = d;
+    if (mode == BIN_TAIL) {
+      if (qn > 0) atomicOr(a.err, ERR_DEPTH);  // level 254 not empty
+      const uint32_t nl = min(d, 255u);
+      for (uint32_t k = 0; k < nl; ++k)
+        __hip_atomic_store(&a.hprof[2 + k], __hip_atomic_load(&a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&a.hprof[1], nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&a.hprof[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     __hip_atomic_store(&hstate[1], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&hstate[0], d, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // the host polls this word
   }
 }
 
+// Level d (pi == BIN_NOPAIR), or pair pi's level dpair[pi] (the predicted loop; no
+// entries there when the BFS already ended). A level below qmin, or any level when no
+// apply follows (binned == 0), runs the direct path here; pair pi then records its next
+// level in dpair[pi + 1] (the apply does when it runs).
 template <int ASZP, class R>
-__global__ __launch_bounds__(512) void k_bin_expand(BinArgs a, uint32_t d, const uint32_t* __restrict__ qcur,
-                                                    uint32_t* __restrict__ qnxt) {
+__global__ __launch_bounds__(512) void k_bin_expand(BinArgs a, uint32_t d, uint32_t pi, uint32_t binned,
+                                                    uint32_t* __restrict__ q0, uint32_t* __restrict__ q1) {
   using RT = typename R::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t qn = a.lvl[d];
-  if (blockIdx.x == 0 && threadIdx.x == 0)  // the host's level poll (host-mapped)
+  if (pi != BIN_NOPAIR) d = a.dpair[pi];
+  const uint32_t qn = d < 254 ? a.lvl[d] : 0u;
+  const uint32_t* __restrict__ qcur = (d & 1) ? q1 : q0;
+  uint32_t* __restrict__ qnxt = (d & 1) ? q0 : q1;
+  if (pi == BIN_NOPAIR && blockIdx.x == 0 && threadIdx.x == 0)  // the host's level poll (host-mapped)
     __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (qn < a.qmin) {
+  if (qn < a.qmin || !binned) {
+    if (pi != BIN_NOPAIR && blockIdx.x == 0 && threadIdx.x == 0) a.dpair[pi + 1] = qn ? d + 1 : d;
     bin_direct<ASZP>(a, d, qn, qcur, qnxt);
     return;
   }
@@ -311,11 +344,15 @@ __host__ __device__ inline size_t bin_apply_lds_bytes(uint32_t BS) {
 }
 
 template <class R>
-__global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t d, uint32_t* __restrict__ qnxt) {
+__global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t d, uint32_t pi, uint32_t* __restrict__ qa,
+                                                            uint32_t* __restrict__ qb) {
   using RT = typename R::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t qn = a.lvl[d];
+  if (pi != BIN_NOPAIR) d = a.dpair[pi];
+  const uint32_t qn = d < 254 ? a.lvl[d] : 0u;
+  uint32_t* __restrict__ qnxt = (d & 1) ? qa : qb;
   if (qn == 0 || qn < a.qmin) return;  // (a direct level: no Lt entry, the gather skips it)
+  if (pi != BIN_NOPAIR && blockIdx.x == 0 && threadIdx.x == 0) a.dpair[pi + 1] = d + 1;
   const uint32_t b = xcd_bin(blockIdx.x, a.nbins);
   if (b >= a.nbins) return;
   const uint32_t tid = threadIdx.x, nb = a.nbins, BP = 1u << a.BS, NW = BP / 32;
@@ -427,10 +464,14 @@ __host__ __device__ inline size_t bin_apply_sb_lds_bytes(uint32_t BS) {
   return 4 * (2 * (size_t)SEG_CHUNK + 1 + 2 * SB_N * (((size_t)1 << BS) / 32) + 2 * SB_N + 64);
 }
 
-__global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply_sb(BinArgs a, uint32_t d, uint32_t* __restrict__ qnxt) {
+__global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply_sb(BinArgs a, uint32_t d, uint32_t pi,
+                                                               uint32_t* __restrict__ qa, uint32_t* __restrict__ qb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t qn = a.lvl[d];
+  if (pi != BIN_NOPAIR) d = a.dpair[pi];
+  const uint32_t qn = d < 254 ? a.lvl[d] : 0u;
+  uint32_t* __restrict__ qnxt = (d & 1) ? qa : qb;
   if (qn == 0 || qn < a.qmin) return;  // (a direct level: no Lt entry, the gather skips it)
+  if (pi != BIN_NOPAIR && blockIdx.x == 0 && threadIdx.x == 0) a.dpair[pi + 1] = d + 1;
   const uint32_t nb = a.nbins, nsb = (nb + SB_N - 1) >> SB_LOG;
   const uint32_t B = xcd_bin(blockIdx.x, nsb);
   if (B >= nsb) return;
@@ -798,46 +839,98 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
   });
   if (r != hipSuccess) return r;
   // Levels of at most `lim` frontier pairs run in one workgroup (k_bin_small); larger ones
-  // as expand + apply, the host enqueueing level d after seeing level d - lag's size
-  // (host-mapped, written by expand) so the GPU never idles for the host's reaction.
+  // as expand (+ apply when binned). Two forms, as in the multi-source BFS: predicted
+  // (a level profile from an earlier round: the head kernel, one expand (+ apply) per
+  // level the profile had above the tail threshold, the tail kernel -- all enqueued at
+  // once, the host never waits) or polled (the host enqueues level d after seeing level
+  // d - lag's size, host-mapped, written by expand).
   volatile uint32_t* hl = e.mv_hlvl;
   volatile uint32_t* hs = e.mv_hlvl + 256;
   uint32_t small = BIN_SMALL;
   if (const char* x = std::getenv("GS_BIN_SMALL")) small = (uint32_t)std::strtoul(x, nullptr, 10);
   if (e.prm.flags & GS_FLAG_NO_SMALL_LEVELS) small = 0;
   const uint32_t lim = std::min(small, a.qmin - 1), lag = 2;
-  uint32_t d = 0;
-  for (;;) {
-    hs[0] = MV_PENDING;
-    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_small<A>), dim3(1), dim3(BIN_ST), 0, e.st, a, d, lim, e.q[0], e.q[1],
-                                                e.mv_hstate_dev));
-    e.bfs_level = d;
-    if ((r = mv_wait(hs, e.st, d))) return r;
-    if (hs[1] == 0) break;
-    const uint32_t dl = d;
-    bool done = false;
-    for (;; ++d) {
-      if (d >= 254) {  // levels through 253 enqueued: the hops fit u8 iff level 254 is empty
-        bool empty = false;
-        if ((r = level_empty(e, 254, empty))) return r;
-        if (!empty) return hipErrorNotSupported;
-        done = true;
-        break;
-      }
-      hl[d] = MV_PENDING;
-      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_expand<A, R>), dim3(xgrid), dim3(xth), lds_x, e.st, a, d,
-                                                  e.q[d & 1], e.q[(d + 1) & 1]));
-      if (SBA) hipLaunchKernelGGL(k_bin_apply_sb, dim3(sbgrid), dim3(APPLY_THREADS), lds_sb, e.st, a, d, e.q[(d + 1) & 1]);
-      else hipLaunchKernelGGL(k_bin_apply<R>, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, e.q[(d + 1) & 1]);
-      if (d >= dl + lag) {
-        uint32_t x = 0;
-        e.bfs_level = d - lag;
-        if ((r = mv_wait(hl + (d - lag), e.st, x))) return r;
-        if (x == 0) { done = true; break; }
-        if (x <= lim) { ++d; break; }  // levels through d are enqueued; small levels from d + 1
+  static const bool polled_only = std::getenv("GS_MV_POLLED") && std::getenv("GS_MV_POLLED")[0] == '1';
+  static const uint32_t tail_thr = [] {
+    const char* x = std::getenv("GS_BIN_TAIL");
+    return x ? (uint32_t)std::strtoul(x, nullptr, 10) : 2048u;
+  }();
+  {  // the newest published profile (a tail kernel of an earlier round)
+    volatile uint32_t* vp = e.mv_prof;
+    const uint32_t sq = vp[0];
+    if (sq != 0 && sq != e.mv_prof_seen[0]) {
+      std::atomic_thread_fence(std::memory_order_acquire);
+      const uint32_t nl = std::min<uint32_t>((uint32_t)vp[1], 255u);
+      std::vector<uint32_t> pv(nl);
+      for (uint32_t k = 0; k < nl; ++k) pv[k] = vp[2 + k];
+      if (vp[0] == sq) {
+        e.mv_pred[0] = std::move(pv);
+        e.mv_prof_seen[0] = sq;
       }
     }
-    if (done) break;
+  }
+  const std::vector<uint32_t>& pv = e.mv_pred[0];
+  const bool predicted = !pv.empty() && !polled_only && lim > 0;
+  if (predicted) {
+    uint32_t k0 = 0;
+    while (k0 < pv.size() && pv[k0] <= lim) ++k0;
+    uint32_t k1 = (uint32_t)pv.size();  // one past the last level above the tail threshold
+    while (k1 > k0 && pv[k1 - 1] <= std::min(tail_thr, lim)) --k1;
+    const uint32_t npairs = std::min<uint32_t>(k1 - k0 + mv_margin(), 250);
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_small<A>), dim3(1), dim3(BIN_ST), 0, e.st, a, BIN_HEAD, 0u, 0u,
+                                                lim, e.q[0], e.q[1], e.mv_hstate_dev, 0u));
+    for (uint32_t i = 0; i < npairs; ++i) {
+      const uint32_t binned = k0 + i < pv.size() && pv[k0 + i] >= a.qmin ? 1u : 0u;  // predicted binned level
+      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_expand<A, R>), dim3(xgrid), dim3(xth), lds_x, e.st, a, 0u, i,
+                                                  binned, e.q[0], e.q[1]));
+      if (binned) {
+        if (SBA) hipLaunchKernelGGL(k_bin_apply_sb, dim3(sbgrid), dim3(APPLY_THREADS), lds_sb, e.st, a, 0u, i, e.q[0], e.q[1]);
+        else hipLaunchKernelGGL(k_bin_apply<R>, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, 0u, i, e.q[0], e.q[1]);
+      }
+    }
+    const uint32_t seq = ++e.mv_seq ? e.mv_seq : ++e.mv_seq;
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_small<A>), dim3(1), dim3(BIN_ST), 0, e.st, a, BIN_TAIL, 0u, npairs,
+                                                lim, e.q[0], e.q[1], e.mv_hstate_dev, seq));
+  } else {
+    uint32_t d = 0, nlev = 0;
+    for (;;) {
+      hs[0] = MV_PENDING;
+      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_small<A>), dim3(1), dim3(BIN_ST), 0, e.st, a, BIN_POLL, d, 0u,
+                                                  lim, e.q[0], e.q[1], e.mv_hstate_dev, 0u));
+      e.bfs_level = d;
+      if ((r = mv_wait(hs, e.st, d))) return r;
+      if (hs[1] == 0) { nlev = d; break; }
+      const uint32_t dl = d;
+      bool done = false;
+      for (;; ++d) {
+        if (d >= 254) {  // levels through 253 enqueued: the hops fit u8 iff level 254 is empty
+          bool empty = false;
+          if ((r = level_empty(e, 254, empty))) return r;
+          if (!empty) return hipErrorNotSupported;
+          nlev = d;
+          done = true;
+          break;
+        }
+        hl[d] = MV_PENDING;
+        GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_expand<A, R>), dim3(xgrid), dim3(xth), lds_x, e.st, a, d,
+                                                    BIN_NOPAIR, 1u, e.q[0], e.q[1]));
+        if (SBA) hipLaunchKernelGGL(k_bin_apply_sb, dim3(sbgrid), dim3(APPLY_THREADS), lds_sb, e.st, a, d, BIN_NOPAIR, e.q[0], e.q[1]);
+        else hipLaunchKernelGGL(k_bin_apply<R>, dim3(bgrid), dim3(APPLY_THREADS), lds_a, e.st, a, d, BIN_NOPAIR, e.q[0], e.q[1]);
+        if (d >= dl + lag) {
+          uint32_t x = 0;
+          e.bfs_level = d - lag;
+          if ((r = mv_wait(hl + (d - lag), e.st, x))) return r;
+          if (x == 0) { nlev = d + 1; done = true; break; }
+          if (x <= lim) { ++d; break; }  // levels through d are enqueued; small levels from d + 1
+        }
+      }
+      if (done) break;
+    }
+    if (!polled_only && lim > 0) {  // this round's sizes seed the prediction
+      std::vector<uint32_t> p2(nlev);
+      for (uint32_t k = 0; k < nlev; ++k) p2[k] = hl[k];
+      e.mv_pred[0] = std::move(p2);
+    }
   }
   if (a.BS <= 11) hipLaunchKernelGGL((k_bin_gather<R, GATHER_THREADS_S>), dim3(bgrid), dim3(GATHER_THREADS_S), lds_g, e.st, a);
   else hipLaunchKernelGGL((k_bin_gather<R, GATHER_THREADS_L>), dim3(bgrid), dim3(GATHER_THREADS_L), lds_g, e.st, a);
@@ -850,7 +943,7 @@ hipError_t launch_bfs_binned(Engine& e, bool record) {
   a.obkt = e.obkt; a.nfail = e.nfail; a.mask = e.mask; a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb;
   a.egress = e.egress; a.egress_acc = e.egress_acc; a.lvl = e.lvl; a.err = e.err; a.area = e.bin_area;
   a.T = e.bin_T; a.pool = e.bin_pool; a.Lt = e.bin_Lt; a.binoff = e.bin_binoff;
-  a.visbm = e.bin_vis; a.hlvl = e.mv_hlvl_dev;
+  a.visbm = e.bin_vis; a.hlvl = e.mv_hlvl_dev; a.dpair = e.mv_dpair; a.hprof = e.mv_prof_dev;
   a.N = e.N; a.ASZ = e.ASZ; a.fanout = e.fanout; a.fc = e.fcap; a.capin = e.capin; a.Gmax = e.bin.Gmax;
   a.PW = e.bin.PW; a.BS = e.bin.BS; a.nbins = e.bin.nbins; a.ORW = e.ORW; a.csr_cap = e.bin.csr_cap;
   a.qmin = (e.prm.flags & GS_FLAG_BINNED_ALL_LEVELS) ? 1u : BIN_MIN_FRONTIER;

@@ -33,6 +33,7 @@
 // to host-mapped memory and the host polls it two levels late (after an event).
 // Results equal k_bfs_level's: hops, in-degrees, inbound record sets, egress.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -49,6 +50,7 @@ constexpr uint32_t MV_XT = 256;       // expand threads = frontier entries per e
 constexpr uint32_t MV_AT = 1024;      // apply threads
 constexpr uint32_t MV_GT = 512;       // gather threads
 constexpr uint32_t MV_SEG = 1024;     // T rows per apply chunk
+constexpr uint32_t MV_NOPAIR = 0xFFFFFFFFu;  // expand / apply: the level is the kernel argument d
 constexpr uint32_t GT_OWN = 0, GT_NOBS = 25, GT_OBV = 26, GT_OBM = 58, GT_NSEED = 90, GT_SEED = 91, GT_S0 = 92,
                    GT_SG = 93;
 
@@ -69,7 +71,9 @@ struct MvArgs {
   uint32_t* err;
   uint32_t* vis;          // [N] slot masks reached
   uint32_t* lvl;          // [256] frontier entries per level
-  uint32_t* hlvl;         // host-mapped [256]: expand(d) writes lvl[d] here
+  uint32_t* hlvl;         // host-mapped [256]: expand(d) writes lvl[d] here (the polled loop)
+  uint32_t* dpair;        // [258] level of expand/apply pair i (predicted loop): head writes [0], apply(i) [i + 1]
+  uint32_t* hprof;        // host-mapped: the tail kernel's level profile (seq, levels, sizes)
   uint32_t* T;            // [rows_cap][TW] rows of the current level
   unsigned long long* area;  // records of the current level
   uint32_t* ctr;          // [0] records used in area (this level)
@@ -228,12 +232,17 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const uint32_
   }
 }
 
+// Level d (pi == MV_NOPAIR), or pair pi's level dpair[pi] (the predicted loop; 0 entries
+// there when the BFS already ended: a no-op).
 template <int ASZP>
-__global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, const uint2* __restrict__ qcur) {
+__global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, uint32_t pi, const uint2* __restrict__ q0,
+                                                     const uint2* __restrict__ q1) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t sorg[32], sfk[32], sbase;
-  const uint32_t qn = a.lvl[d];
-  if (blockIdx.x == 0 && threadIdx.x == 0)  // the host's termination poll (host-mapped)
+  if (pi != MV_NOPAIR) d = a.dpair[pi];
+  const uint32_t qn = d < 254 ? a.lvl[d] : 0u;
+  const uint2* __restrict__ qcur = (d & 1) ? q1 : q0;
+  if (pi == MV_NOPAIR && blockIdx.x == 0 && threadIdx.x == 0)  // the host's termination poll (host-mapped)
     __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint32_t G = (qn + MV_XT - 1) / MV_XT;
   if (blockIdx.x >= G) return;  // idle workgroups leave before any setup
@@ -301,31 +310,39 @@ __host__ __device__ inline size_t mv_apply_lds_bytes(uint32_t BSC) {
 // Node v's new slots as frontier entries, one per distinct entry k: slots whose origin
 // bucket is >= bucket[v] share v's own entry, the rest split by origin bucket. Returns
 // the entry count; writes them at out[pos..] when out != nullptr.
-__device__ inline uint32_t mv_parts(const uint32_t* gt, uint32_t v, uint32_t nw, uint32_t bv, uint2* out,
-                                    uint32_t pos) {
+template <class Put>
+__device__ inline uint32_t mv_parts_to(const uint32_t* gt, uint32_t v, uint32_t nw, uint32_t bv, Put put) {
   uint32_t n = 0;
   const uint32_t own = nw & gt[GT_OWN + bv];
-  if (own) {
-    if (out) out[pos] = make_uint2(v | (bv << 24), own);
-    ++n;
-  }
+  if (own) put(n++, make_uint2(v | (bv << 24), own));
   const uint32_t rest = nw & ~own;
   if (rest) {
     const uint32_t nobs = gt[GT_NOBS];
     for (uint32_t i = 0; i < nobs; ++i) {
       const uint32_t m = rest & gt[GT_OBM + i];
-      if (!m) continue;
-      if (out) out[pos + n] = make_uint2(v | (gt[GT_OBV + i] << 24), m);
-      ++n;
+      if (m) put(n++, make_uint2(v | (gt[GT_OBV + i] << 24), m));
     }
   }
   return n;
 }
 
-__global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint2* __restrict__ qnxt) {
+__device__ inline uint32_t mv_parts(const uint32_t* gt, uint32_t v, uint32_t nw, uint32_t bv, uint2* out,
+                                    uint32_t pos) {
+  return mv_parts_to(gt, v, nw, bv, [&](uint32_t k, uint2 x) {
+    if (out) out[pos + k] = x;
+  });
+}
+
+__global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32_t pi, uint2* __restrict__ q0,
+                                                   uint2* __restrict__ q1) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t qn = a.lvl[d];
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[0] = 0;  // expand(d) is done with it; expand(d + 1) starts at 0
+  if (pi != MV_NOPAIR) d = a.dpair[pi];
+  const uint32_t qn = d < 254 ? a.lvl[d] : 0u;
+  uint2* __restrict__ qnxt = (d & 1) ? q0 : q1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.ctr[0] = 0;  // expand(d) is done with it; expand(d + 1) starts at 0
+    if (pi != MV_NOPAIR) a.dpair[pi + 1] = qn ? d + 1 : d;
+  }
   if (qn == 0) return;
   const uint32_t c = mv_xcd_bin(blockIdx.x, a.nbc);
   if (c >= a.nbc) return;
@@ -435,26 +452,43 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint2*
 // ------------------------------------------------------------ small levels ----
 constexpr uint32_t MV_ST = 1024;     // threads of the small-level workgroup
 constexpr uint32_t MV_SMALL_LP = 8192;  // fine bins up to which the small kernel keeps pool fills in LDS
-constexpr uint32_t MV_SMALL = 1024;  // frontier entries at most for a small level (default; GS_MV_SMALL): C4 917 us vs 936 at 4096
+constexpr uint32_t MV_SMALL = 1024;  // frontier entries at most for a head level (default; GS_MV_SMALL)
+constexpr uint32_t MV_SQ = 2048;     // frontier entries of a level kept in the small kernel's LDS queue
+enum : uint32_t { MV_HEAD = 0, MV_TAIL = 1, MV_POLL = 2 };  // small-kernel modes
 
 template <class T>
 __device__ inline T mv_ld(T* p) {  // device-scope load: lines updated by atomics elsewhere
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Levels with at most MV_SMALL frontier entries run inside ONE workgroup, level after
-// level, with no launch between them: every entry is expanded (mv_expand_entry), each
-// record ORs its slots into vis with a device-scope atomic -- the atomic that sets a
-// slot's bit is that slot's first arrival (hop d + 1, gossip.rs:594-600) -- new bits
-// become next-level entries, and the record is appended to its fine bin's pool run
-// (one atomic per record: few records). Starts at level d0; stops at the first level
-// with no entries or more than MV_SMALL; writes (level, entries) to hstate.
+// A barrier for LDS only: global stores in flight are not waited for (nothing in the level
+// loop reads another thread's global stores; vis is read by atomics only).
+__device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Levels run inside ONE workgroup, level after level, with no launch between them: every
+// entry is expanded (mv_expand_entry), each record ORs its slots into vis with a
+// device-scope atomic -- the atomic that sets a slot's bit is that slot's first arrival
+// (hop d + 1, gossip.rs:594-600) -- new bits become next-level entries (an LDS queue of
+// MV_SQ entries, the rest in global memory), and the record is appended to its fine bin's
+// pool run. Modes:
+//   MV_HEAD  the round's first levels: seeds the group (lvl, pool fills, vis of the seed
+//            nodes, the first queue), runs while a level has at most a.small entries,
+//            leaves the level where it stopped in dpair[0] for the expand/apply pairs;
+//   MV_TAIL  from level dpair[pi] to the end of the BFS whatever the level sizes (the host
+//            enqueued pairs by the previous round's level profile; a level the pairs did not
+//            take is expanded here, slowly but correctly); writes the round's level profile
+//            to host-mapped memory (hprof) for the next round's prediction;
+//   MV_POLL  from level d0 while levels have at most a.small entries (the polled loop).
+// Every mode reports (level, entries) where it stopped in hstate.
 template <int ASZP>
-__global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2* __restrict__ q0,
-                                                    uint2* __restrict__ q1, uint32_t* __restrict__ hstate) {
+__global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uint32_t d0, uint32_t pi,
+                                                    uint2* __restrict__ q0, uint2* __restrict__ q1,
+                                                    uint32_t* __restrict__ hstate, const uint2* __restrict__ seeds,
+                                                    uint32_t nseed, uint32_t seq) {
   // [fno] pool fill at level start, then (when LP) [fno] the running fill: the records'
   // pool places come from LDS atomics, the global fills are written once at the end
   extern __shared__ __attribute__((aligned(16))) uint32_t snap[];
+  __shared__ uint2 qL[2][MV_SQ];
   __shared__ uint32_t sorg[32], sfk[32], gt[GT_WORDS], cnt_s;
   const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BPm = (1u << BSC) - 1;
   const bool LP = a.fno <= MV_SMALL_LP;  // (uniform)
@@ -464,25 +498,66 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2
     sfk[tid] = a.fk[a.s0 + tid];
   }
   for (uint32_t i = tid; i < GT_WORDS; i += MV_ST) gt[i] = a.gt[i];
-  for (uint32_t f = tid; f < a.fno; f += MV_ST) {
-    snap[f] = mv_ld(&a.pused[f]);
-    if (LP) lp[f] = snap[f];
+  uint32_t d = mode == MV_TAIL ? a.dpair[pi] : d0;
+  bool inL = false;  // the current level's entries [0, MV_SQ) are in qL[d & 1]
+  if (mode == MV_HEAD) {  // the group's round starts here: no memsets of lvl / pool fills, no seed launch
+    for (uint32_t i = tid; i < 256; i += MV_ST) a.lvl[i] = i == 0 ? nseed : 0u;
+    for (uint32_t f = tid; f < a.fno; f += MV_ST) {
+      a.pused[f] = 0;
+      snap[f] = 0;
+      if (LP) lp[f] = 0;
+    }
+    if (tid == 0) a.ctr[0] = 0;
+    if (tid < nseed) {
+      const uint2 sd = seeds[tid];  // distinct origins (vis was cleared before this kernel)
+      qL[0][tid] = sd;
+      a.vis[sd.x & 0xFFFFFFu] = sd.y;
+    }
+    inL = true;
+    __syncthreads();  // (full: the seeds' vis stores land before any vis atomic)
+  } else {
+    for (uint32_t f = tid; f < a.fno; f += MV_ST) {
+      snap[f] = mv_ld(&a.pused[f]);
+      if (LP) lp[f] = snap[f];
+    }
   }
-  uint32_t d = d0, qn = a.lvl[d0];
-  while (qn > 0 && qn <= a.small && d < 254) {
-    uint2* qcur = (d & 1) ? q1 : q0;
-    uint2* qnxt = (d & 1) ? q0 : q1;
+  // GS_PHASE_PROFILE: section clocks of thread 0 at pclk[0..4] (setup, expand loads,
+  // atomics + places, Lt + barrier; [4] levels)
+  unsigned long long tm = a.pclk && tid == 0 ? wall_clock64() : 0;
+  auto mark = [&](int ph) {
+    if (a.pclk && tid == 0) {
+      const unsigned long long now = wall_clock64();
+      atomicAdd(&a.pclk[ph], now - tm);
+      tm = now;
+    }
+  };
+  uint32_t qn = mode == MV_HEAD ? nseed : (d < 256 ? a.lvl[d] : 0u);
+  const uint32_t lim = mode == MV_TAIL ? 0xFFFFFFFFu : a.small;
+  __syncthreads();
+  mark(0);
+  while (qn > 0 && qn <= lim && d < 254) {
+    const uint2* qg = (d & 1) ? q1 : q0;
+    uint2* qgn = (d & 1) ? q0 : q1;
+    const uint2* ql = qL[d & 1];
+    uint2* qln = qL[(d + 1) & 1];
     if (tid == 0) {
       cnt_s = 0;
-      __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (a.pclk) atomicAdd(&a.pclk[4], 1ull);
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t i0 = 0; i0 < qn; i0 += MV_ST) {
       const uint32_t i = i0 + tid;
       uint32_t row[ASZP], acc[ASZP], u = 0;
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
-      if (i < qn) mv_expand_entry<ASZP>(a, qcur[i], sorg, sfk, row, acc, u);
+      if (i < qn) mv_expand_entry<ASZP>(a, inL && i < MV_SQ ? ql[i] : qg[i], sorg, sfk, row, acc, u);
+      if (a.pclk && i0 == 0) {  // (profiling only: wait for the entry's loads)
+        uint32_t x = 0;
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s) x |= acc[s];
+        if (x == 0xFFFFFFFFu) atomicOr(a.err, 0u);
+        mark(1);
+      }
       // every global access of the entry is issued before any result is used (one wait,
       // not one round trip per pushed-to peer): the vis atomics, the peers' buckets and,
       // without LDS fills, the pool-place atomics
@@ -513,12 +588,19 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2
         if (nw) {  // this thread's first arrivals at w (another thread may add more bits to w)
           const uint32_t n = mv_parts(gt, w, nw, bw[s], nullptr, 0);
           const uint32_t base = atomicAdd(&cnt_s, n);
-          if ((size_t)base + n <= a.q_cap) mv_parts(gt, w, nw, bw[s], qnxt, base);
-          else atomicOr(a.err, ERR_MV_CAP);
+          if ((size_t)base + n <= a.q_cap) {
+            mv_parts_to(gt, w, nw, bw[s], [&](uint32_t k, uint2 x) {
+              if (base + k < MV_SQ) qln[base + k] = x;
+              else qgn[base + k] = x;
+            });
+          } else {
+            atomicOr(a.err, ERR_MV_CAP);
+          }
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
+    mark(2);
     for (uint32_t f = tid; f < a.fno; f += MV_ST) {  // the level's pool run of every kept fine bin
       const uint32_t now = LP ? lp[f] : mv_ld(&a.pused[f]);
       a.Lt[(size_t)d * a.fno + f] = make_uint2(snap[f], now - snap[f]);
@@ -527,14 +609,33 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t d0, uint2
     qn = min(cnt_s, (uint32_t)a.q_cap);
     ++d;
     if (tid == 0) a.lvl[d] = qn;
-    __syncthreads();
+    inL = true;
+    if (qn > MV_SQ) __syncthreads();  // (entries beyond the LDS queue went to global memory)
+    else lds_barrier();
+    mark(3);
   }
   if (LP)
     for (uint32_t f = tid; f < a.fno; f += MV_ST) a.pused[f] = lp[f];
+  if (qn > 0 && inL && mode != MV_TAIL) {  // the next level's entries for expand: the LDS part to global memory
+    uint2* qg = (d & 1) ? q1 : q0;
+    for (uint32_t i = tid; i < min(qn, MV_SQ); i += MV_ST) qg[i] = qL[d & 1][i];
+  }
+  if (mode == MV_TAIL && qn > 0 && tid == 0) atomicOr(a.err, ERR_DEPTH);  // level 254 not empty
   if (tid == 0) {
+    if (mode == MV_HEAD) a.dpair[0] = d;
+    if (mode == MV_TAIL) {  // the round's level profile for the host's next prediction
+      uint32_t* hp = a.hprof;
+      const uint32_t nl = min(d, 255u);
+      for (uint32_t k = 0; k < nl; ++k) __hip_atomic_store(&hp[2 + k], a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&hp[1], nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&hp[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     __hip_atomic_store(&hstate[1], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&hstate[0], d, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // the host polls this word
   }
+  if (tid == 0 && mode != MV_TAIL)  // per-level sizes for the polled loop / diagnostics (tid 0 wrote lvl[])
+    for (uint32_t k = d0; k < d && k < 256; ++k)
+      __hip_atomic_store(&a.hlvl[k], a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // --------------------------------------------------------------- gather ----
@@ -931,19 +1032,6 @@ __global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void
   if (errf) atomicOr(a.err, errf);
 }
 
-__global__ void k_mv_seed(MvArgs a, const uint2* __restrict__ seeds, uint32_t nseed, uint2* __restrict__ q0) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nseed) {
-    const uint2 s = seeds[i];
-    q0[i] = s;
-    a.vis[s.x & 0xFFFFFFu] = s.y;  // seed nodes are distinct origins
-  }
-  if (i == 0) {
-    a.lvl[0] = nseed;
-    a.ctr[0] = 0;
-  }
-}
-
 // fcls[w] = smallest i (1-based) with frank[w] < T[i-1] over the ascending distinct
 // failure counts T[0..m); 255 when w fails in no slot.
 __global__ void k_mv_fcls(const uint32_t* __restrict__ frank, const uint32_t* __restrict__ T, uint32_t m, uint32_t N,
@@ -1067,6 +1155,7 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.origin = e.origin; a.mask = e.mask; a.gt = e.mv_gtab + (size_t)g * GT_WORDS;
   a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb; a.egress = e.egress; a.err = e.err;
   a.vis = e.mv_vis; a.lvl = e.lvl; a.hlvl = e.mv_hlvl_dev; a.T = e.mv_T; a.area = e.mv_area; a.ctr = e.mv_ctr;
+  a.dpair = e.mv_dpair; a.hprof = nullptr;
   a.pool = e.mv_pool; a.pused = e.mv_pused; a.Lt = e.mv_Lt;
   a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
@@ -1130,11 +1219,69 @@ hipError_t level_empty(Engine& e, uint32_t d, bool& empty) {
   return r;
 }
 
+// The level loop of one slot group. Two forms:
+//  - predicted (the group has a level profile from an earlier round): everything is
+//    enqueued at once and the host never waits -- the head kernel (seed + levels of at
+//    most a.small entries), one expand/apply pair per level the profile had above the
+//    tail threshold (each pair reads its level from dpair on the device, so a pair past
+//    the BFS's end is a no-op), and the tail kernel, which finishes the BFS whatever is
+//    left (and publishes this round's profile). Levels per round barely change between
+//    rounds (the active sets rotate slowly), so the pairs fit.
+//  - polled (no profile yet): the host enqueues level d after seeing level d - lag's size.
+static hipError_t mv_group_polled(Engine& e, MvArgs& a, const MvGroup& gr, uint32_t lag, uint32_t& nlev) {
+  hipError_t r;
+  const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)MV_XT * e.ASZP * 8;
+  const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
+  const uint32_t fno = mv_kept_bins(e);
+  const size_t lds_s = (size_t)fno * (fno <= MV_SMALL_LP ? 8 : 4);
+  const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8, xgrid = 2048;
+  volatile uint32_t* hl = e.mv_hlvl;        // host-mapped: expand(d) writes lvl[d]
+  volatile uint32_t* hs = e.mv_hlvl + 256;  // host-mapped: the small-level kernel's (level, entries)
+  uint32_t d = 0;
+  bool head = true;
+  for (;;) {
+    // small levels in one workgroup, until the frontier is empty or large
+    hs[0] = MV_PENDING;
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a,
+                                                head ? MV_HEAD : MV_POLL, d, 0u, e.mv_q[0], e.mv_q[1],
+                                                e.mv_hstate_dev, e.mv_seed + gr.seed0, gr.nseed, 0u));
+    head = false;
+    e.bfs_level = d;
+    if ((r = mv_wait(hs, e.st, d))) return r;
+    if (hs[1] == 0) { nlev = d; return hipSuccess; }
+    if (d >= 254) return hipErrorNotSupported;  // frontier still non-empty after 254 levels
+    // large levels: expand + apply; the frontier size of level x is polled `lag` levels late
+    const uint32_t dl = d;
+    for (;; ++d) {
+      if (d >= 254) {  // levels through 253 enqueued: the hops fit u8 iff level 254 is empty
+        bool empty = false;
+        if ((r = level_empty(e, 254, empty))) return r;
+        if (!empty) return hipErrorNotSupported;
+        nlev = d;
+        return hipSuccess;
+      }
+      hl[d] = MV_PENDING;
+      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, d,
+                                                  MV_NOPAIR, e.mv_q[0], e.mv_q[1]));
+      hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, d, MV_NOPAIR, e.mv_q[0], e.mv_q[1]);
+      if (d >= dl + lag) {
+        uint32_t x = 0;
+        e.bfs_level = d - lag;
+        if ((r = mv_wait(hl + (d - lag), e.st, x))) return r;
+        if (x == 0) { nlev = d + 1; return hipSuccess; }
+        if (x <= a.small) { ++d; break; }  // levels d - 1, d are enqueued; small levels from d + 1
+      }
+    }
+  }
+}
+
 hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
   hipError_t r = hipSuccess;
   const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)MV_XT * e.ASZP * 8;
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
   const size_t lds_g = MV_GLDS;
+  const uint32_t fno = mv_kept_bins(e);
+  const size_t lds_s = (size_t)fno * (fno <= MV_SMALL_LP ? 8 : 4);
   if (!e.mv_attr_set) {
     GS_ASZP_DISPATCH(e.ASZP, {
       r = hipFuncSetAttribute((const void*)k_mv_expand<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
@@ -1147,70 +1294,72 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     if ((r = hipFuncSetAttribute((const void*)k_mv_consume, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g)))
       return r;
     GS_ASZP_DISPATCH(e.ASZP, {
-      r = hipFuncSetAttribute((const void*)k_mv_small<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(mv_kept_bins(e) * (mv_kept_bins(e) <= MV_SMALL_LP ? 8 : 4)));
+      r = hipFuncSetAttribute((const void*)k_mv_small<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s);
     });
     if (r != hipSuccess) return r;
     e.mv_attr_set = true;
   }
   const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8;
-  const uint32_t fno = mv_kept_bins(e);
   const uint32_t ggrid = ((fno + 7) / 8) * 8;
   const uint32_t xgrid = 2048;
-  volatile uint32_t* hl = e.mv_hlvl;  // host-mapped: expand(d) writes lvl[d]
-  volatile uint32_t* hs = e.mv_hlvl + 256;  // host-mapped: the small-level kernel's (level, entries)
-  const size_t lds_s = (size_t)fno * (fno <= MV_SMALL_LP ? 8 : 4);
-  // the host enqueues level d after seeing level d - lag's frontier size (levels past the
-  // end run as no-ops); a short lag left the GPU idle for the host's reaction at every
-  // short tail level
   uint32_t lag = 2;
   if (const char* x = std::getenv("GS_MV_LAG")) lag = std::max<uint32_t>(1, (uint32_t)std::strtoul(x, nullptr, 10));
+  static const bool polled_only = std::getenv("GS_MV_POLLED") && std::getenv("GS_MV_POLLED")[0] == '1';
+  static const uint32_t tail_thr = [] {  // levels the profile had at or below this run in the tail kernel
+    const char* x = std::getenv("GS_MV_TAIL");
+    return x ? (uint32_t)std::strtoul(x, nullptr, 10) : 2048u;
+  }();
   for (uint32_t g = 0; g < (uint32_t)e.mv_groups.size(); ++g) {
     const MvGroup& gr = e.mv_groups[g];
     MvArgs a = mv_args(e, gr, g);
     a.record = record ? 1u : 0u;
+    uint32_t* hp = e.mv_prof + (size_t)g * MV_PROF_WORDS;
+    a.hprof = e.mv_prof_dev + (size_t)g * MV_PROF_WORDS;
+    {  // the newest published profile of this group (a tail kernel of an earlier round)
+      volatile uint32_t* vp = hp;
+      const uint32_t sq = vp[0];
+      if (sq != e.mv_prof_seen[g] && sq != 0) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        const uint32_t nl = std::min<uint32_t>((uint32_t)vp[1], 255u);
+        std::vector<uint32_t> pv(nl);
+        for (uint32_t k = 0; k < nl; ++k) pv[k] = vp[2 + k];
+        if (vp[0] == sq) {  // (not rewritten meanwhile)
+          e.mv_pred[g] = std::move(pv);
+          e.mv_prof_seen[g] = sq;
+        }
+      }
+    }
     hipEvent_t t0;
     e.tbegin("bfs", &t0);
     if ((r = hipMemsetAsync(e.mv_vis, 0, (size_t)e.N * 4, e.st))) return r;
-    if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st))) return r;
-    if ((r = hipMemsetAsync(e.mv_pused, 0, (size_t)fno * 4, e.st))) return r;
-    hipLaunchKernelGGL(k_mv_seed, dim3((gr.nseed + 255) / 256), dim3(256), 0, e.st, a, e.mv_seed + gr.seed0, gr.nseed,
-                       e.mv_q[0]);
-    uint32_t nlev = 0, d = 0;
-    for (;;) {
-      // small levels in one workgroup, until the frontier is empty or large
-      hs[0] = MV_PENDING;
-      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, d,
-                                                  e.mv_q[0], e.mv_q[1], e.mv_hstate_dev));
-      e.bfs_level = d;
-    if ((r = mv_wait(hs, e.st, d))) return r;
-      if (hs[1] == 0) { nlev = d; break; }
-      if (d >= 254) return hipErrorNotSupported;  // frontier still non-empty after 254 levels
-      // large levels: expand + apply; the frontier size of level x is polled two levels late
-      const uint32_t dl = d;
-      bool done = false;
-      for (;; ++d) {
-        if (d >= 254) {  // levels through 253 enqueued: the hops fit u8 iff level 254 is empty
-          bool empty = false;
-          if ((r = level_empty(e, 254, empty))) return r;
-          if (!empty) return hipErrorNotSupported;
-          nlev = d;
-          done = true;
-          break;
-        }
-        hl[d] = MV_PENDING;
-        GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, d,
-                                                    e.mv_q[d & 1]));
-        hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, d, e.mv_q[(d + 1) & 1]);
-        if (d >= dl + lag) {
-          uint32_t x = 0;
-          e.bfs_level = d - lag;
-        if ((r = mv_wait(hl + (d - lag), e.st, x))) return r;
-          if (x == 0) { nlev = d + 1; done = true; break; }
-          if (x <= a.small) { ++d; break; }  // levels d - 1, d are enqueued; small levels from d + 1
-        }
+    uint32_t nlev = 254;  // (the gather reads the levels' sizes; empty levels end the BFS)
+    const std::vector<uint32_t>& pv = e.mv_pred[g];
+    if (pv.empty() || polled_only || e.mv_diag) {
+      if ((r = mv_group_polled(e, a, gr, lag, nlev))) return r;
+      if (!polled_only) {  // this round's sizes seed the prediction
+        std::vector<uint32_t> p2(nlev);
+        for (uint32_t k = 0; k < nlev; ++k) p2[k] = e.mv_hlvl[k];
+        e.mv_pred[g] = std::move(p2);
       }
-      if (done) break;
+    } else {
+      // the head kernel stops at the first level above a.small; pairs then take the levels
+      // the profile had above the tail threshold
+      uint32_t k0 = 0;
+      while (k0 < pv.size() && pv[k0] <= a.small) ++k0;
+      uint32_t k1 = (uint32_t)pv.size();  // one past the last level above the tail threshold
+      while (k1 > k0 && pv[k1 - 1] <= tail_thr) --k1;
+      const uint32_t npairs = std::min<uint32_t>(k1 - k0 + mv_margin(), 250);
+      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, MV_HEAD, 0u,
+                                                  0u, e.mv_q[0], e.mv_q[1], e.mv_hstate_dev, e.mv_seed + gr.seed0,
+                                                  gr.nseed, 0u));
+      for (uint32_t i = 0; i < npairs; ++i) {
+        GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, 0u,
+                                                    i, e.mv_q[0], e.mv_q[1]));
+        hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, 0u, i, e.mv_q[0], e.mv_q[1]);
+      }
+      const uint32_t seq = ++e.mv_seq ? e.mv_seq : ++e.mv_seq;  // (never 0)
+      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, MV_TAIL, 0u,
+                                                  npairs, e.mv_q[0], e.mv_q[1], e.mv_hstate_dev, nullptr, 0u, seq));
     }
     e.tend("bfs", t0);
     e.tbegin(consume ? "gather_consume" : "gather", &t0);
@@ -1221,11 +1370,21 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       std::vector<uint32_t> pu(fno);
       if ((r = hipMemcpyAsync(pu.data(), e.mv_pused, pu.size() * 4, hipMemcpyDeviceToHost, e.st))) return r;
       if ((r = hipStreamSynchronize(e.st))) return r;
+      volatile uint32_t* hl = e.mv_hlvl;
       size_t ent = 0, rec = 0, mx = 0;
       for (uint32_t d = 0; d < nlev; ++d) ent += hl[d];
       for (uint32_t x : pu) { rec += x; mx = std::max<size_t>(mx, x); }
       std::fprintf(stderr, "GS_MV_DIAG group %u: levels %u, entries %zu, records %zu (max %zu per fine bin)\n", g,
                    nlev, ent, rec, mx);
+      std::vector<uint2> lt((size_t)nlev * fno);
+      if ((r = hipMemcpy(lt.data(), e.mv_Lt, lt.size() * sizeof(uint2), hipMemcpyDeviceToHost))) return r;
+      std::fprintf(stderr, "GS_MV_DIAG levels (entries/records):");
+      for (uint32_t d = 0; d < nlev; ++d) {
+        size_t rd = 0;
+        for (uint32_t f = 0; f < fno; ++f) rd += lt[(size_t)d * fno + f].y;
+        std::fprintf(stderr, " %u/%zu", hl[d], rd);
+      }
+      std::fprintf(stderr, "\n");
     }
   }
   return hipGetLastError();

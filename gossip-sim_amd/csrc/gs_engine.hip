@@ -82,6 +82,7 @@ static void destroy_engine(Engine* e) {
   if (e->h_err) hipHostFree(e->h_err);
   if (e->part_in) hipFree(e->part_in);
   if (e->mv_hlvl) hipHostFree(e->mv_hlvl);
+  if (e->mv_prof) hipHostFree(e->mv_prof);
   for (auto& kv : e->timers)
     for (auto& pr : kv.second.ev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (hipEvent_t x : e->ev_pool) hipEventDestroy(x);
@@ -328,6 +329,17 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
       return fail(GS_ENOMEM, "host-mapped frontier counters");
     }
     e->mv_hstate_dev = e->mv_hlvl_dev + 256;
+    // the predicted level loops: per-pair levels, and one level profile per slot group
+    ALLOC(e->mv_dpair, 258, 0);
+    const size_t ng = mode == GS_BFS_MULTI ? (S + e->mv.GW - 1) / e->mv.GW : 1;
+    if (hipHostMalloc(&e->mv_prof, ng * MV_PROF_WORDS * 4, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&e->mv_prof_dev, e->mv_prof, 0) != hipSuccess) {
+      destroy_engine(e);
+      return fail(GS_ENOMEM, "host-mapped level profiles");
+    }
+    std::memset(e->mv_prof, 0, ng * MV_PROF_WORDS * 4);
+    e->mv_pred.assign(ng, {});
+    e->mv_prof_seen.assign(ng, 0);
   }
   if (mode == GS_BFS_MULTI) {
     const MvGeom& g = e->mv;
@@ -494,6 +506,13 @@ int gs_set_slots(gs_engine* eh, const gs_slot* slots, uint32_t n_slots) {
     HIPC(hipMemcpyAsync(e->mv_gtab, gtab.data(), gtab.size() * 4, hipMemcpyHostToDevice, e->st));
     HIPC(hipMemcpyAsync(e->mv_seed, seeds.data(), seeds.size() * sizeof(uint2), hipMemcpyHostToDevice, e->st));
   }
+  if (e->mv_prof) {  // new origins: no level profile to predict from (earlier rounds' are ignored)
+    HIPC(hipStreamSynchronize(e->st));
+    for (size_t g = 0; g < e->mv_pred.size(); ++g) {
+      e->mv_pred[g].clear();
+      e->mv_prof_seen[g] = ((volatile uint32_t*)e->mv_prof)[g * MV_PROF_WORDS];
+    }
+  }
   e->slots.assign(slots, slots + n_slots);
   e->slots_set = true;
   int r = reset_pair_state(e);
@@ -581,6 +600,11 @@ int gs_fail_nodes(gs_engine* eh, const double* fraction) {
     e->h_nfail_any[o] = nf[o] ? 1u : 0u;
   }
   HIPC(mv_update_failures(*e, nf));
+  for (auto& pv : e->mv_pred) pv.clear();  // failures reshape the levels: the next round polls again
+  if (e->mv_prof) {  // (and ignores profiles published before now)
+    const size_t ng = e->mv_pred.size();
+    for (size_t g = 0; g < ng; ++g) e->mv_prof_seen[g] = ((volatile uint32_t*)e->mv_prof)[g * MV_PROF_WORDS];
+  }
   HIPC(hipMemcpyAsync(e->nfail, nf.data(), e->S * 4, hipMemcpyHostToDevice, e->st));
   HIPC(hipStreamSynchronize(e->st));
   return GS_OK;

@@ -1,5 +1,6 @@
 // gs_internal.h -- engine state shared by the kernels' launchers and the C ABI.
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <map>
@@ -121,6 +122,12 @@ struct Engine {
   uint32_t* mv_hlvl = nullptr;    // host-mapped [256] frontier sizes (host pointer)
   uint32_t* mv_hlvl_dev = nullptr;  // its device pointer
   uint32_t* mv_hstate_dev = nullptr;  // device pointer of mv_hlvl + 256 (small-level kernel's state)
+  uint32_t* mv_dpair = nullptr;   // [258] level of each expand/apply pair of the predicted loop
+  uint32_t* mv_prof = nullptr;    // host-mapped [groups][MV_PROF_WORDS]: the tail kernel's level profile
+  uint32_t* mv_prof_dev = nullptr;
+  std::vector<std::vector<uint32_t>> mv_pred;  // per group: the last known level sizes (empty: none yet)
+  std::vector<uint32_t> mv_prof_seen;          // per group: the profile sequence number last read
+  uint32_t mv_seq = 0;                         // profile sequence numbers handed to the tail kernels
   uint32_t* mv_gtab = nullptr;    // [groups][GT_WORDS]
   uint2* mv_seed = nullptr;       // [S] seed entries (distinct origins) of every group
   std::vector<MvGroup> mv_groups;
@@ -202,6 +209,17 @@ hipError_t launch_bfs_binned(Engine& e, bool record);
 // spin on a host-mapped word the device writes (MV_PENDING until then); checks the stream
 // now and then so a stream that ended without writing it fails instead of hanging
 constexpr uint32_t MV_PENDING = 0xFFFFFFFFu;
+constexpr uint32_t MV_PROF_WORDS = 258;  // seq, levels, sizes of levels 0..255
+// Extra expand/apply pairs the predicted level loops enqueue beyond the profile's levels
+// (no-ops when the BFS ends as predicted; they take a level the profile did not expect
+// instead of the one-workgroup tail kernel). GS_MV_MARGIN, default 1.
+inline uint32_t mv_margin() {
+  static const uint32_t m = [] {
+    const char* x = std::getenv("GS_MV_MARGIN");
+    return x ? (uint32_t)std::strtoul(x, nullptr, 10) : 1u;
+  }();
+  return m;
+}
 hipError_t mv_wait(volatile uint32_t* p, hipStream_t st, uint32_t& out);  // bounded: hipErrorLaunchTimeOut
 // after the level loop enqueued levels through d - 1: is level d's frontier empty (syncs the stream)
 hipError_t level_empty(Engine& e, uint32_t d, bool& empty);

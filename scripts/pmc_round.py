@@ -42,11 +42,22 @@ def main():
     ap.add_argument("--marker", default="k_mv_gather")
     ap.add_argument("--rounds", default="5,24")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--all", action="store_true",
+                    help="every round of the run (engines interleaved): family total / marker dispatches")
     a = ap.parse_args()
     fam = a.family.split(",")
     r0, r1 = (int(x) for x in a.rounds.split(","))
-    f = per_round(load(os.path.join(a.dir, "fetch", "run_counter_collection.csv"), "FETCH_SIZE"), fam, a.marker, r0, r1)
-    w = per_round(load(os.path.join(a.dir, "write", "run_counter_collection.csv"), "WRITE_SIZE"), fam, a.marker, r0, r1)
+    fr = load(os.path.join(a.dir, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    wr = load(os.path.join(a.dir, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    if a.all:
+        def whole(rows):
+            n = sum(1 for _, k, _ in rows if a.marker in k)
+            return sum(v for _, k, v in rows if any(x in k for x in fam)) / n
+        f, w = whole(fr), whole(wr)
+        r0, r1 = "all", "all"
+    else:
+        f = per_round(fr, fam, a.marker, r0, r1)
+        w = per_round(wr, fam, a.marker, r0, r1)
     out = {"kernels": fam, "rounds": [r0, r1], "fetch_size_kib_raw_per_round": f, "write_size_kib_raw_per_round": w,
            "fetch_bytes_corrected": f * 1024 * 2, "write_bytes": w * 1024,
            "traffic_bytes_per_launch": f * 1024 * 2 + w * 1024, "launch": "one round of the family",

@@ -226,8 +226,8 @@ def test_round_by_round_parity_level_kernels(mode, extra):
 
 @pytest.mark.parametrize("mode", [gs.GS_BFS_BINNED, gs.GS_BFS_MULTI])
 def test_parity_hub_in_degrees_above_64(mode):
-    """Fanout = active-set size 32 on 500 nodes whose stakes halve every 8 ranks (buckets
-    24 down to 0), inbound capacity 256: the top-stake nodes sit in most high-bucket
+    """Fanout = active-set size 32 on 500 nodes whose stakes halve every 8 stake ranks (buckets
+    24 down to 0; stake ranks shuffled over the ids), inbound capacity 256: the top-stake nodes sit in most high-bucket
     entries and receive 65-83 pushes a round -- the binned gather's whole-wave rows for
     pairs above G_HEAVY = 64 records, the consume's single-lane path above 64 -- every
     level binned; against the oracle round by round. (The binned gather's fallback for a
@@ -235,6 +235,7 @@ def test_parity_hub_in_degrees_above_64(mode):
     above 32 >= fanout.)"""
     n = 500
     st = np.maximum(2.0 ** (54 - np.arange(n) / 8.0), 1e9).astype(np.uint64)
+    st = st[np.random.default_rng(5).permutation(n)]  # hubs spread over the ids (and the multi BFS's fine bins)
     extra = dict(inbound_capacity=256, binned_all_levels=mode == gs.GS_BFS_BINNED)
     eng, sims, origins, _ = make_pair(n, [1], asz=32, fanout=32, p=0.05, mode=mode, extra=extra, stakes=st)
     eng.run_gossip()
