@@ -640,7 +640,14 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
 
 // --------------------------------------------------------------- gather ----
 constexpr uint32_t MV_GC = 12;        // records per gather thread kept in registers between the passes
-constexpr uint32_t MV_GLDS = 78 * 1024;  // gather LDS: two workgroups per CU
+constexpr uint32_t MV_GLDS_DEF = 78 * 1024;  // gather LDS: two workgroups per CU (GS_MV_GLDS_KB: tuning)
+static uint32_t mv_glds() {
+  static const uint32_t v = [] {
+    const char* x = std::getenv("GS_MV_GLDS_KB");
+    return x ? std::min<uint32_t>(160, std::max<uint32_t>(16, (uint32_t)std::strtoul(x, nullptr, 10))) * 1024u : MV_GLDS_DEF;
+  }();
+  return v;
+}
 constexpr uint32_t MV_WSCR = 64 + CACHE_CAP;  // fused consume: per-wave LDS scratch (u32)
 constexpr uint32_t MV_CSCR = (MV_GT / 64) * MV_WSCR * 4;  // bytes of all waves' scratch
 
@@ -1079,8 +1086,8 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   const size_t rpn = (size_t)ASZ * std::min<size_t>(sg, 4) + 16;  // pool records per node (average over a bin)
   g.pcap = ((size_t)1 << g.BSF) * rpn;
   // (4 records' worth of slack: the filters read up to 3 records past a node's list)
-  g.gcap = (uint32_t)((MV_GLDS - mv_gather_fixed_bytes(g.BSF)) / 8) - 4;
-  g.gcap_c = (uint32_t)((MV_GLDS - MV_CSCR - mv_gather_fixed_bytes(g.BSF)) / 8) - 4;
+  g.gcap = (uint32_t)((mv_glds() - mv_gather_fixed_bytes(g.BSF)) / 8) - 4;
+  g.gcap_c = (uint32_t)((mv_glds() - MV_CSCR - mv_gather_fixed_bytes(g.BSF)) / 8) - 4;
 }
 
 bool mv_supported(const MvGeom& g, uint32_t ASZP) {
@@ -1279,7 +1286,7 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
   hipError_t r = hipSuccess;
   const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)MV_XT * e.ASZP * 8;
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
-  const size_t lds_g = MV_GLDS;
+  const size_t lds_g = mv_glds();
   const uint32_t fno = mv_kept_bins(e);
   const size_t lds_s = (size_t)fno * (fno <= MV_SMALL_LP ? 8 : 4);
   if (!e.mv_attr_set) {
