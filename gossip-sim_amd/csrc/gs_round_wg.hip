@@ -211,7 +211,7 @@ __device__ inline void match_pairs(const uint32_t (&pk)[8], uint32_t k2, uint32_
 
 // ---- C: register path (1 <= c <= 16) ----
 __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t* recs, const uint8_t* hops_l,
-                                    uint32_t c, uint32_t& len, uint32_t& up, uint32_t& errf, uint32_t rm) {
+                                    uint32_t c, uint32_t& len, uint32_t& up, uint32_t& errf) {
   const size_t PAIRS = a.PAIRS;
   const uint32_t q = (uint32_t)p;
   uint32_t rk[16];
@@ -220,7 +220,7 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
   for (int j = 0; j < 16; ++j) {
     rk[j] = 0xFFFFFFFFu;
     if ((uint32_t)j < wc) {
-      const uint32_t s = recs[min((uint32_t)j, c - 1)] & rm;
+      const uint32_t s = recs[min((uint32_t)j, c - 1)];
       const uint32_t key = ((uint32_t)hops_l[s] << 16) | s;  // (hop, id): hop = dist[src] + 1 shifts all alike
       rk[j] = (uint32_t)j < c ? key : 0xFFFFFFFFu;
     }
@@ -289,18 +289,9 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
 
 // ---- D: register path (len <= 32). Rows are rewritten in prune order with the
 // pruned flag; returns the number of prunees. ----
-// The prune pass's register path (len <= 16). With 12-bit ids (N <= 4,096, rings of <= 16
-// slots: k12) the sort key carries the node id -- (127 - score) << 24 | prank << 12 | id --
-// so no by-rank id lookup follows the sort; the by-id prune ranks come from an LDS table
-// (prk_l), stakes only until the prune tail starts (the cumulative stake never decreases
-// after it). PushActiveSet::prune needs the pruner v's ring slot in the prunee u's entry:
-// when u pushed to v this round (nearly always: active sets rotate slowly) v's CSR list
-// carries it (records are src | ring slot << 12), else u's row is loaded (apply_prune_r).
-// Without k12: global prank / by_prank lookups and the row path.
 template <int ASZP>
 __device__ inline uint32_t prune_lane(const RoundArgs& a, uint32_t* mkw, const uint16_t* nl_l, uint32_t org, size_t p,
-                                      uint32_t v, uint32_t len, uint32_t mi, uint64_t mis, const uint16_t* prk_l,
-                                      bool k12, const uint16_t* vrec, uint32_t vc) {
+                                      uint32_t v, uint32_t len, uint32_t mi, uint64_t mis) {
   const size_t PAIRS = a.PAIRS;
   const uint32_t q = (uint32_t)p;
   const uint32_t wl = active_max<5>(len);
@@ -311,10 +302,7 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, uint32_t* mkw, const u
     asm volatile("" ::: "memory");
     uint32_t pr[LANE_L];
 #pragma unroll
-    for (int i = 0; i < LANE_L; ++i) {
-      const uint32_t id = (uint32_t)i < len ? ck_id(sk[i]) : 0u;
-      pr[i] = (uint32_t)i < wl ? (k12 ? ((uint32_t)prk_l[id] << 12) | id : a.prank[id]) : 0u;
-    }
+    for (int i = 0; i < LANE_L; ++i) pr[i] = (uint32_t)i < wl ? a.prank[(uint32_t)i < len ? ck_id(sk[i]) : 0u] : 0u;
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = 0; i < LANE_L; ++i)
@@ -324,6 +312,7 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, uint32_t* mkw, const u
   else sort_net<LANE_L>(sk);
   // sorted_unstable_by_key(Reverse((score, stake))), ties by id; scan of pre-add
   // cumulative stake; skip(min_ingress_nodes); skip_while(cum < min_ingress_stake).
+  // Node ids and stakes of 8 sorted entries at a time are gathered with one wait.
   uint64_t cum = 0;
   uint32_t npr = 0;
   bool tail = false;
@@ -334,10 +323,9 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, uint32_t* mkw, const u
     uint64_t st[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      const uint32_t i = c0 + t, x = i < len ? sk[c0 + t] : 0u;
-      const uint32_t r = k12 ? (x >> 12) & 0xFFFu : x & 0xFFFFFFu;
-      nd[t] = k12 ? x & 0xFFFu : a.by_prank[r];
-      st[t] = tail ? 0ull : a.pstake[r];  // (past the prune tail's start stakes are not needed)
+      const uint32_t i = c0 + t, r = i < len ? sk[c0 + t] & 0xFFFFFFu : 0u;
+      nd[t] = a.by_prank[r];
+      st[t] = a.pstake[r];
     }
     asm volatile("" ::: "memory");
 #pragma unroll
@@ -348,21 +336,7 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, uint32_t* mkw, const u
         const bool pruned = tail && nd[t] != org;
         npr += pruned;
         nts(&(a.ckey + (size_t)i * PAIRS)[q], ck_make(nd[t], (0x7Fu - (sk[c0 + t] >> 24)) | (pruned ? PRUNED_FLAG : 0u)));
-        if (pruned) {  // prune_connections
-          uint32_t sl = 0xFFu;
-          if (k12)
-            for (uint32_t k = 0; k < vc; ++k) {
-              const uint32_t r = vrec[k];
-              if ((r & 0xFFFu) == nd[t]) sl = r >> 12;
-            }
-          if (sl != 0xFFu) {
-            const uint32_t u = nd[t];
-            if (ASZP <= 16) atomicOr(&mkw[u >> 1], (1u << sl) << ((u & 1u) << 4));
-            else atomicOr(&mkw[u], 1u << sl);
-          } else {
-            apply_prune_r<ASZP>(a, mkw, nl_l, nd[t], v);
-          }
-        }
+        if (pruned) apply_prune_r<ASZP>(a, mkw, nl_l, nd[t], v);  // prune_connections
         cum = sat_add(cum, st[t]);
       }
     }
@@ -372,13 +346,13 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, uint32_t* mkw, const u
 
 // ---- C: wave path (16 < c <= 64), all 64 lanes on one node; len/up uniform ----
 __device__ inline void consume_wave(const RoundArgs& a, size_t p, const uint16_t* recs, const uint8_t* hops_l,
-                                    uint32_t c, uint32_t& len, uint32_t& up, uint32_t* scr, uint32_t& errf, uint32_t rm) {
+                                    uint32_t c, uint32_t& len, uint32_t& up, uint32_t* scr, uint32_t& errf) {
   const size_t PAIRS = a.PAIRS;
   const uint32_t q = (uint32_t)p;
   const uint32_t l = lane_id();
   uint32_t key = 0xFFFFFFFFu;
   if (l < c) {
-    const uint32_t s = recs[l] & rm;
+    const uint32_t s = recs[l];
     key = ((uint32_t)hops_l[s] << 16) | s;
   }
 #pragma unroll
@@ -427,7 +401,7 @@ __device__ inline void consume_wave(const RoundArgs& a, size_t p, const uint16_t
 
 // ---- C: any in-degree (c > 64): lane 0 of the wave, records selected in order ----
 __device__ inline void consume_serial(const RoundArgs& a, size_t p, const uint16_t* recs, const uint8_t* hops_l,
-                                      uint32_t c, uint32_t& len, uint32_t& up, uint32_t& errf, uint32_t rm) {
+                                      uint32_t c, uint32_t& len, uint32_t& up, uint32_t& errf) {
   const size_t PAIRS = a.PAIRS;
   const uint32_t l = lane_id();
   uint32_t ln = len, u = up;
@@ -437,7 +411,7 @@ __device__ inline void consume_serial(const RoundArgs& a, size_t p, const uint16
     for (uint32_t k = 0; k < c; ++k) {
       uint32_t best = 0xFFFFFFFFu;
       for (uint32_t j = 0; j < c; ++j) {
-        const uint32_t s = recs[j] & rm;
+        const uint32_t s = recs[j];
         const uint32_t key = ((uint32_t)hops_l[s] << 16) | s;
         if ((k == 0 || key > prev) && key < best) best = key;
       }
@@ -662,10 +636,6 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
 
   const uint32_t o = blockIdx.x;
   const uint32_t org = a.origin[o], ob = a.obkt[o], nf = a.nfail[o];
-  // 12-bit ids and rings of <= 16 slots: CSR records carry the push's ring slot
-  // (src | slot << 12), read by the prune pass; rm masks the id out of a record
-  const bool k12 = N <= 4096 && ASZP <= 16;
-  const uint32_t rm = k12 ? 0xFFFu : 0xFFFFu;
   const size_t base = (size_t)o * N;
   uint32_t errf = 0;
   unsigned long long t_mark = PROF && a.phase_clk && tid == 0 ? wall_clock64() : 0;
@@ -875,14 +845,9 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
 #pragma unroll
       for (int j = 0; j < FP; ++j)
         pos[j] = off_fetch_inc<OFF16>(offw, (pk[i][j >> 1] >> ((j & 1) * 16)) & 0xFFFFu, (uint32_t)j < kk[i], dummy);
-      uint32_t pmr = k12 ? (uint32_t)pm_l[v] : 0u;  // list order = ring-slot order (the prepass)
 #pragma unroll
       for (int j = 0; j < FP; ++j)
-        if ((uint32_t)j < kk[i]) {
-          const uint32_t sl = pmr ? (uint32_t)__builtin_ctz(pmr) : 0u;
-          pmr &= pmr - 1;
-          rec_l[pos[j]] = (uint16_t)(v | (sl << 12));
-        }
+        if ((uint32_t)j < kk[i]) rec_l[pos[j]] = (uint16_t)v;
     }
   } else {
     uint32_t* dummy = scr + lane;
@@ -906,21 +871,12 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
         for (int j = 0; j < FP; ++j) p0[j] = off_fetch_inc<OFF16>(offw, d0[j], (uint32_t)j < k0, dummy);
 #pragma unroll
         for (int j = 0; j < FP; ++j) p1[j] = off_fetch_inc<OFF16>(offw, d1[j], (uint32_t)j < k1, dummy);
-        uint32_t m0 = k12 ? pm0 : 0u, m1 = k12 ? pm1 : 0u;  // ring slots in push order
 #pragma unroll
         for (int j = 0; j < FP; ++j)
-          if ((uint32_t)j < k0) {
-            const uint32_t sl = m0 ? (uint32_t)__builtin_ctz(m0) : 0u;
-            m0 &= m0 - 1;
-            rec_l[p0[j]] = (uint16_t)(v0 | (sl << 12));
-          }
+          if ((uint32_t)j < k0) rec_l[p0[j]] = (uint16_t)v0;
 #pragma unroll
         for (int j = 0; j < FP; ++j)
-          if ((uint32_t)j < k1) {
-            const uint32_t sl = m1 ? (uint32_t)__builtin_ctz(m1) : 0u;
-            m1 &= m1 - 1;
-            rec_l[p1[j]] = (uint16_t)(v1 | (sl << 12));
-          }
+          if ((uint32_t)j < k1) rec_l[p1[j]] = (uint16_t)v1;
       }
     }
   }
@@ -942,11 +898,17 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
       continue;
     }
     uint32_t len = meta & 0xFF, up = (meta >> 8) & 0xFF;
-    if (c) consume_lane(a, p, rec_l + (off_l[v] - c), hops_l, c, len, up, errf, rm);
-    if (up >= MIN_NUM_UPSERTS) {  // due: pruned below (long entries by a wave, the rest in the prune pass)
-      nts(&a.cmeta[p], len | (up << 8));
-      if (len > (uint32_t)LANE_L) hv_l[N - 1 - atomicAdd(&ctrl[C_NHP], 1u)] = (uint16_t)v;
-      else atomicOr(&bm_l[v >> 5], 1u << (v & 31));  // (bm_l: the due set until the prune pass)
+    if (c) consume_lane(a, p, rec_l + (off_l[v] - c), hops_l, c, len, up, errf);
+    if (up >= MIN_NUM_UPSERTS) {
+      if (len > (uint32_t)LANE_L) {
+        nts(&a.cmeta[p], len | (up << 8));
+        hv_l[N - 1 - atomicAdd(&ctrl[C_NHP], 1u)] = (uint16_t)v;
+        continue;
+      }
+      const uint64_t sv = a.stake[v];
+      const uint32_t npr = prune_lane<ASZP>(a, mkw, nl_l, org, p, v, len, mi, min_ingress_stake(sv < so ? sv : so, rwg_thr(a, o)));
+      npr_sum += npr;
+      finish_node(a, p, meta, len, 0, npr, true);
     } else {
       finish_node(a, p, meta, len, up, 0, false);
     }
@@ -966,8 +928,8 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
       if (is_c) {
         const uint32_t c = cnt_l[v];
         const uint16_t* recs = rec_l + (off_l[v] - c);
-        if (c <= a.wave_c_max) consume_wave(a, p, recs, hops_l, c, len, up, scr, errf, rm);
-        else consume_serial(a, p, recs, hops_l, c, len, up, errf, rm);
+        if (c <= a.wave_c_max) consume_wave(a, p, recs, hops_l, c, len, up, scr, errf);
+        else consume_serial(a, p, recs, hops_l, c, len, up, errf);
       }
       const bool due = up >= MIN_NUM_UPSERTS;
       uint32_t npr = 0;
@@ -977,37 +939,6 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
         if (lane == 0) npr_sum += npr;
       }
       if (lane == 0) finish_node(a, p, meta, len, due ? 0u : up, npr, due);
-    }
-  }
-  // ---------------- D: the prune pass (lane path) ------------------------------
-  // Entries reaching 20 upserts come in waves (every node of a slot in the same round),
-  // so the pass costs nothing in other rounds. With k12 the by-id prune ranks are an
-  // LDS table over the heavy-node list's area (dead now); the CSR is still intact.
-  {
-    uint32_t any = 0;
-    const uint32_t W = (N + 31) / 32;
-    for (uint32_t i = tid; i < W; i += RWG_THREADS) any |= bm_l[i];
-    if (__syncthreads_or(any != 0)) {
-      uint16_t* prk_l = reinterpret_cast<uint16_t*>(smem + L.pm);
-      if (k12) {
-        for (uint32_t i = tid; i < N; i += RWG_THREADS) prk_l[i] = (uint16_t)a.prank[i];
-        __syncthreads();
-      }
-      for (uint32_t v = tid; v < N; v += RWG_THREADS) {
-        if (!((bm_l[v >> 5] >> (v & 31)) & 1u)) continue;
-        const size_t p = base + v;
-        const uint32_t meta = a.cmeta[p];  // (this thread's own store above)
-        const uint32_t len = meta & 0xFF, c = cnt_l[v];
-        const uint64_t sv = a.stake[v];
-        const uint32_t npr = prune_lane<ASZP>(a, mkw, nl_l, org, p, v, len, mi,
-                                              min_ingress_stake(sv < so ? sv : so, rwg_thr(a, o)), prk_l, k12,
-                                              rec_l + (off_l[v] - c), c);
-        npr_sum += npr;
-        finish_node(a, p, meta, len, 0, npr, true);
-      }
-      __syncthreads();
-      for (uint32_t i = tid; i < W; i += RWG_THREADS) bm_l[i] = 0;  // (the stranded bitmap below)
-      __syncthreads();
     }
   }
   if (npr_sum) atomicAdd(&ctrl[C_PRUNES], npr_sum);

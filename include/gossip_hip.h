@@ -191,6 +191,7 @@ int gs_engine_round_kind(gs_engine* e, uint32_t* fused);
  * [node_lo, node_hi) (gs_part_sizes): K contiguous ranges of whole 1,024-id bins of
  * C = ceil(n / K) rounded up to 1,024; every rank must own a node ((K - 1) * C < n, else
  * gs_create_part fails with GS_EINVAL on the empty ranks -- check before creating).
+ * K = 1 gives one rank owning every node (the exchange calls work; a one-rank group). 
  * Replicated on every rank: active sets, prune masks, failed flags (the same rotations,
  * failures and prune bits are applied everywhere). Kept for owned nodes only: every
  * per-(slot, node) array -- hops, in-degrees, received caches, round counters,
