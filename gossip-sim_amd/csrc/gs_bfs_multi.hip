@@ -73,6 +73,7 @@ struct MvArgs {
   uint32_t* lvl;          // [256] frontier entries per level
   uint32_t* hlvl;         // host-mapped [256]: expand(d) writes lvl[d] here (the polled loop)
   uint32_t* dpair;        // [258] level of expand/apply pair i (predicted loop): head writes [0], apply(i) [i + 1]
+  uint32_t* snapg;        // [fno] small-level kernel: level-start pool fills when they do not fit LDS
   uint32_t* hprof;        // host-mapped: the tail kernel's level profile (seq, levels, sizes)
   uint32_t* T;            // [rows_cap][TW] rows of the current level
   unsigned long long* area;  // records of the current level
@@ -487,12 +488,14 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
                                                     uint32_t nseed, uint32_t seq) {
   // [fno] pool fill at level start, then (when LP) [fno] the running fill: the records'
   // pool places come from LDS atomics, the global fills are written once at the end
-  extern __shared__ __attribute__((aligned(16))) uint32_t snap[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t snap_l[];
   __shared__ uint2 qL[2][MV_SQ];
   __shared__ uint32_t sorg[32], sfk[32], gt[GT_WORDS], cnt_s;
   const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BPm = (1u << BSC) - 1;
   const bool LP = a.fno <= MV_SMALL_LP;  // (uniform)
-  uint32_t* lp = snap + a.fno;
+  // (beyond MV_SMALL_LP fine bins the level-start fills live in global memory: a.snapg)
+  uint32_t* snap = LP ? snap_l : a.snapg;
+  uint32_t* lp = snap_l + a.fno;
   if (tid < a.Sg) {
     sorg[tid] = a.origin[a.s0 + tid];
     sfk[tid] = a.fk[a.s0 + tid];
@@ -1075,6 +1078,8 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   g.BSF = std::min(g.BSC, 9u);  // fine bins of <= 512 nodes (gather at C4: 301 vs 412 us with 1,024)
   // (GS_MV_BSF: tuning; at most 10 so that a partition range of whole 1,024-id bins is whole fine bins)
   if (const char* x = std::getenv("GS_MV_BSF")) g.BSF = std::min(std::min(g.BSC, 10u), std::max(6u, (uint32_t)std::strtoul(x, nullptr, 10)));
+  // apply keeps one LDS cursor per fine bin of its coarse bin: at most 16 (k_mv_apply's fcur)
+  g.BSF = std::max(g.BSF, g.BSC > 4 ? g.BSC - 4 : 0u);
   g.nbc = (N + (1u << g.BSC) - 1) >> g.BSC;
   g.nbf = g.nbc << (g.BSC - g.BSF);
   g.GW = std::min(28u, (64u - g.UB - g.BSC) & ~3u);
@@ -1162,7 +1167,7 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.origin = e.origin; a.mask = e.mask; a.gt = e.mv_gtab + (size_t)g * GT_WORDS;
   a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb; a.egress = e.egress; a.err = e.err;
   a.vis = e.mv_vis; a.lvl = e.lvl; a.hlvl = e.mv_hlvl_dev; a.T = e.mv_T; a.area = e.mv_area; a.ctr = e.mv_ctr;
-  a.dpair = e.mv_dpair; a.hprof = nullptr;
+  a.dpair = e.mv_dpair; a.hprof = nullptr; a.snapg = e.mv_snapg;
   a.pool = e.mv_pool; a.pused = e.mv_pused; a.Lt = e.mv_Lt;
   a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
@@ -1240,7 +1245,7 @@ static hipError_t mv_group_polled(Engine& e, MvArgs& a, const MvGroup& gr, uint3
   const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)MV_XT * e.ASZP * 8;
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
   const uint32_t fno = mv_kept_bins(e);
-  const size_t lds_s = (size_t)fno * (fno <= MV_SMALL_LP ? 8 : 4);
+  const size_t lds_s = fno <= MV_SMALL_LP ? (size_t)fno * 8 : 0;
   const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8, xgrid = 2048;
   volatile uint32_t* hl = e.mv_hlvl;        // host-mapped: expand(d) writes lvl[d]
   volatile uint32_t* hs = e.mv_hlvl + 256;  // host-mapped: the small-level kernel's (level, entries)
@@ -1288,7 +1293,7 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
   const size_t lds_g = mv_glds();
   const uint32_t fno = mv_kept_bins(e);
-  const size_t lds_s = (size_t)fno * (fno <= MV_SMALL_LP ? 8 : 4);
+  const size_t lds_s = fno <= MV_SMALL_LP ? (size_t)fno * 8 : 0;
   if (!e.mv_attr_set) {
     GS_ASZP_DISPATCH(e.ASZP, {
       r = hipFuncSetAttribute((const void*)k_mv_expand<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);

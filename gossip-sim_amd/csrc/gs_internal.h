@@ -123,6 +123,7 @@ struct Engine {
   uint32_t* mv_hlvl_dev = nullptr;  // its device pointer
   uint32_t* mv_hstate_dev = nullptr;  // device pointer of mv_hlvl + 256 (small-level kernel's state)
   uint32_t* mv_dpair = nullptr;   // [258] level of each expand/apply pair of the predicted loop
+  uint32_t* mv_snapg = nullptr;   // [kept fine bins] the small-level kernel's fills beyond its LDS
   uint32_t* mv_prof = nullptr;    // host-mapped [groups][MV_PROF_WORDS]: the tail kernel's level profile
   uint32_t* mv_prof_dev = nullptr;
   std::vector<std::vector<uint32_t>> mv_pred;  // per group: the last known level sizes (empty: none yet)

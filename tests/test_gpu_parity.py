@@ -665,6 +665,31 @@ def _invariants(eng, k, n, summ_last, failed=None):
     return hops
 
 
+def test_multi_bfs_many_fine_bins_matches_level():
+    """More fine bins than the small-level kernel keeps in LDS (4.2M nodes in 512-node fine
+    bins: 8,204 > 8,192): its level-start pool fills live in global memory and its pool
+    places are global atomics. Four rounds with failures, three slots, through the
+    predicted level loop from round 1: equal to the level BFS (summaries, hops, counters)."""
+    n = 4_200_000
+    st = eb.synth.power_law_stakes(n)
+    m = gs.Engine(st, 3, seed=29, rotation_probability=0.01, bfs_mode=gs.GS_BFS_MULTI)
+    lv = gs.Engine(st, 3, seed=29, rotation_probability=0.01, bfs_mode=gs.GS_BFS_LEVEL)
+    for e in (m, lv):
+        e.set_slots([0, 0, 5], [2, 2, 1], [0.15, 0.3, 0.15])
+        e.init_active_sets()
+        e.fail_nodes([0.0, 0.2, 0.1])
+    for r in range(4):
+        for e in (m, lv):
+            e.round(r, record=True)
+    np.testing.assert_array_equal(m.summaries(), lv.summaries())
+    for k in range(3):
+        np.testing.assert_array_equal(m.hops(k), lv.hops(k))
+        for x, y in zip(m.counters(k), lv.counters(k)):
+            np.testing.assert_array_equal(x, y)
+    for e in (m, lv):
+        e.close()
+
+
 def test_c4_sweep_slots_1m():
     """BASELINE C4 at size: a 1M-node power-law network, origin rank 1, the fail-nodes sweep
     (f = 0.1..0.5, when-to-fail 0) and the prune-stake-threshold sweep (0.05..0.40) as 13
