@@ -223,6 +223,54 @@ __device__ inline uint32_t prune_lane(const CgArgs& a, uint32_t q, uint32_t o, u
   return npr;
 }
 
+// A wave's deferred prunes, four lanes per prune: lane j of a quad loads 16 B of the prunee's
+// own-bucket row (words 4j..4j+3; its one 64-B line holds the ring, hl | bucket << 16 in
+// word ASZP, and the failure classes), the quad ORs its ring-slot hits, and one lane sets
+// the mask bits. One coalesced line per prune instead of five scattered loads per lane
+// (bucket, three row quads, hl): a prune wave is bound by the texture address unit's
+// per-lane work (profiles/r03/pmc_prune_c4.txt: TA busy 84 % of the kernel). A prunee
+// whose entry for this origin is not its own bucket (origin bucket below it) takes
+// apply_prune.
+template <int ASZP>
+__device__ inline void apply_prunes_quad(const CgArgs& a, const PruneList& pl, uint32_t pn, uint32_t qb) {
+  static_assert(ASZP % 4 == 0 && ASZP <= 12, "one quad of lanes covers the ring and word ASZP");
+  constexpr uint32_t NQ = ASZP / 4 + 1;
+  const uint32_t l = lane_id(), sub = l & 3u, lead = l & ~3u;
+  for (uint32_t k0 = 0; k0 < pn; k0 += 16) {
+    const uint32_t k = k0 + (l >> 2);
+    const bool ok = k < pn;
+    uint32_t u = 0, v = 0, po = 0;
+    if (ok) {
+      u = pl.u[k];
+      const uint32_t pq = qb + pl.lane[k];
+      po = pq / a.NP;
+      v = a.vlo + (pq - po * a.NP);
+    }
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    if (ok && sub < NQ) w = reinterpret_cast<const uint4*>(a.own + (size_t)u * a.ORW)[sub];
+    const uint32_t wm = (uint32_t)__shfl((int)w.x, (int)(lead | (ASZP / 4)));  // word ASZP
+    const uint32_t head = wm & 0xFFu, L = (wm >> 8) & 0xFFu, bu = wm >> 16;
+    const uint32_t rw[4] = {w.x, w.y, w.z, w.w};
+    uint32_t hit = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t s = sub * 4 + (uint32_t)j;
+      const uint32_t pos = s >= head ? s - head : s + a.ASZ - head;
+      hit |= (uint32_t)(sub < ASZP / 4 && s < a.ASZ && pos < L && rw[j] == v) << s;
+    }
+    hit |= (uint32_t)__shfl_xor((int)hit, 1);
+    hit |= (uint32_t)__shfl_xor((int)hit, 2);
+    if (ok && sub == 0) {
+      const uint32_t ob = a.obkt[po];
+      if (ob >= bu) {
+        if (hit) atomicOr(&a.mask[po * a.mso + u * a.msu], hit);
+      } else {
+        apply_prune<ASZP>(a, po, ob, u, v);
+      }
+    }
+  }
+}
+
 // ---- prune, wave path (32 < len <= 96): two entries per lane ----
 template <int ASZP>
 __device__ inline uint32_t prune_wave(const CgArgs& a, uint32_t q, uint32_t o, uint32_t v, uint32_t len) {
@@ -379,11 +427,17 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const uint32_t qb = p0 + (wid << 6);
-      for (uint32_t k = lane_id(); k < pn; k += 64) {
-        const uint32_t pq = qb + pl.lane[k];
-        const uint32_t po = pq / a.NP;
-        apply_prune<ASZP>(a, po, a.obkt[po], pl.u[k], a.vlo + (pq - po * a.NP));
+      bool quad = false;
+      if constexpr (ASZP <= 12) {
+        quad = a.own != nullptr;
+        if (quad) apply_prunes_quad<ASZP>(a, pl, pn, qb);
       }
+      if (!quad)
+        for (uint32_t k = lane_id(); k < pn; k += 64) {
+          const uint32_t pq = qb + pl.lane[k];
+          const uint32_t po = pq / a.NP;
+          apply_prune<ASZP>(a, po, a.obkt[po], pl.u[k], a.vlo + (pq - po * a.NP));
+        }
       __builtin_amdgcn_wave_barrier();  // the list is reused by the wave's next pairs
     }
     uint64_t hv = __ballot(heavy);
