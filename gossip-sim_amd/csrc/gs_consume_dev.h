@@ -13,12 +13,13 @@ namespace gs {
 template <class T>
 __device__ inline T ntl(const T* p) { return __builtin_nontemporal_load(p); }
 
-// The first 8 cache rows of the lane's pair (rows >= len are not loaded): issued before
-// the records are sorted, so the sort hides their latency.
+// The first 8 cache rows of the lane's pair (rows >= len are not loaded and read as ~0,
+// whose id CK_ID is no node's: n_nodes <= 2^24 - 1): issued before the records are
+// sorted, so the sort hides their latency.
 __device__ inline void cache_prefetch(const uint32_t* __restrict__ ckey, size_t PAIRS, size_t q, uint32_t len,
                                       uint32_t (&kc)[8]) {
 #pragma unroll
-  for (int t = 0; t < 8; ++t) kc[t] = (uint32_t)t < len ? ntl(&(ckey + (size_t)t * PAIRS)[q]) : 0u;
+  for (int t = 0; t < 8; ++t) kc[t] = (uint32_t)t < len ? ntl(&(ckey + (size_t)t * PAIRS)[q]) : 0xFFFFFFFFu;
 }
 
 template <int NC>
@@ -32,13 +33,13 @@ __device__ inline void cache_match(uint32_t* __restrict__ ckey, size_t PAIRS, si
       for (int t = 0; t < 8; ++t) kc[t] = kc0[t];
     } else {
 #pragma unroll
-      for (int t = 0; t < 8; ++t) kc[t] = i0 + t < len ? ntl(&(ckey + (size_t)(i0 + t) * PAIRS)[q]) : 0u;
+      for (int t = 0; t < 8; ++t) kc[t] = i0 + t < len ? ntl(&(ckey + (size_t)(i0 + t) * PAIRS)[q]) : 0xFFFFFFFFu;
     }
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const uint32_t i = i0 + t;
-      const uint32_t k = i < len ? ck_id(kc[t]) : 0xFFFFFFFFu;
+      const uint32_t k = ck_id(kc[t]);  // CK_ID past len: matches no record id
 #pragma unroll
       for (int j = 0; j < NC; ++j) pr[j] = pr[j] || rid[j] == k;
       if (rid[0] == k) { idx0 = (int)i; w0 = kc[t]; }

@@ -158,6 +158,7 @@ __device__ inline void prune_ranks(const CgArgs& a, uint32_t q, uint32_t o, uint
                                    uint32_t len, uint32_t mi, uint64_t mis, const uint32_t (&kk)[LANE_L],
                                    const uint32_t (&nd)[LANE_L], const uint64_t (&st)[LANE_L], PruneList& pl,
                                    uint32_t& npr) {
+  uint32_t rk[W], ow[W];
 #pragma unroll
   for (int i = 0; i < W; ++i) {
     uint32_t rank = 0;
@@ -170,7 +171,8 @@ __device__ inline void prune_ranks(const CgArgs& a, uint32_t q, uint32_t o, uint
     }
     const bool live = (uint32_t)i < len;
     const bool pruned = live && rank >= mi && cum >= mis && nd[i] != org;
-    if (live) (a.ckey + (size_t)rank * a.PAIRS)[q] = ck_make(nd[i], (0x7Fu - (kk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
+    rk[i] = rank;
+    ow[i] = ck_make(nd[i], (0x7Fu - (kk[i] >> 24)) | (pruned ? PRUNED_FLAG : 0u));
     npr += pruned ? 1u : 0u;
     const uint64_t pb = __ballot(pruned);
     if (pruned) {
@@ -183,6 +185,15 @@ __device__ inline void prune_ranks(const CgArgs& a, uint32_t q, uint32_t o, uint
       }
     }
     pl.n += (uint32_t)__popcll(pb);
+  }
+  // the rows rewritten position by position: every lane stores to row p together (one
+  // coalesced store per position instead of a lane-scattered store per entry)
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) w = rk[i] == (uint32_t)p ? ow[i] : w;
+    if ((uint32_t)p < len) (a.ckey + (size_t)p * a.PAIRS)[q] = w;
   }
 }
 

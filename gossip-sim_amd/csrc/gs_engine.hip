@@ -287,6 +287,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   ALLOC(e->by_prank, N, 0);
   ALLOC(e->pstake, N, 0);
   ALLOC(e->pinfo, N, 0);
+  ALLOC(e->rinfo, N, 0);
   ALLOC(e->origin, S, 0);
   ALLOC(e->obkt, S, 0);
   ALLOC(e->min_ingress, S, 0);
@@ -420,13 +421,16 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     for (uint32_t i = 0; i < n; ++i) ids[i] = i;
     std::stable_sort(ids.begin(), ids.end(), [&](uint32_t x, uint32_t y) { return stakes[x] > stakes[y]; });
     for (uint32_t r = 0; r < n; ++r) { pr[ids[r]] = r; ps[r] = stakes[ids[r]]; }
-    std::vector<uint4> pi(N);
-    for (uint32_t i = 0; i < n; ++i)
+    std::vector<uint4> pi(N), ri(N);
+    for (uint32_t i = 0; i < n; ++i) {
       pi[i] = make_uint4(pr[i], 0u, (uint32_t)stakes[i], (uint32_t)(stakes[i] >> 32));
+      ri[i] = make_uint4(ids[i], 0u, (uint32_t)ps[i], (uint32_t)(ps[i] >> 32));
+    }
     if (hipMemcpyAsync(e->prank, pr.data(), N * 4, hipMemcpyHostToDevice, e->st) != hipSuccess ||
         hipMemcpyAsync(e->by_prank, ids.data(), N * 4, hipMemcpyHostToDevice, e->st) != hipSuccess ||
         hipMemcpyAsync(e->pstake, ps.data(), N * 8, hipMemcpyHostToDevice, e->st) != hipSuccess ||
         hipMemcpyAsync(e->pinfo, pi.data(), N * 16, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+        hipMemcpyAsync(e->rinfo, ri.data(), N * 16, hipMemcpyHostToDevice, e->st) != hipSuccess ||
         hipStreamSynchronize(e->st) != hipSuccess) {
       destroy_engine(e);
       return fail(GS_EHIP, "prune-rank upload");

@@ -73,6 +73,7 @@ struct Engine {
   uint32_t* by_prank = nullptr;
   uint64_t* pstake = nullptr;    // stake by prune rank
   uint4* pinfo = nullptr;        // by node id: {prune rank, 0, stake lo, stake hi} (one load per cache key)
+  uint4* rinfo = nullptr;        // by prune rank: {node id, 0, stake lo, stake hi} (the round kernel's sorted entries)
   // slot arrays
   uint32_t* origin = nullptr;
   uint8_t* obkt = nullptr;

@@ -62,6 +62,7 @@ struct RoundArgs {
   const uint32_t* prank;     // rank by (stake desc, id asc): the prune order's tie-broken stake key
   const uint32_t* by_prank;
   const uint64_t* pstake;    // stake by prune rank
+  const uint4* rinfo;        // by prune rank: {node id, 0, stake lo, stake hi}
   const uint32_t* origin;
   const uint8_t* obkt;
   const uint32_t* nfail;
@@ -324,8 +325,9 @@ __device__ inline uint32_t prune_lane(const RoundArgs& a, uint32_t* mkw, const u
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const uint32_t i = c0 + t, r = i < len ? sk[c0 + t] & 0xFFFFFFu : 0u;
-      nd[t] = a.by_prank[r];
-      st[t] = a.pstake[r];
+      const uint4 x = a.rinfo[r];  // node id and stake in one load
+      nd[t] = x.x;
+      st[t] = ((uint64_t)x.w << 32) | x.z;
     }
     asm volatile("" ::: "memory");
 #pragma unroll
@@ -1064,7 +1066,7 @@ static hipError_t launch_rwg(Engine& e, const RoundArgs& a, size_t lds) {
 hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_slot, bool rot_clear) {
   RoundArgs a;
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.frank = e.frank; a.srank = e.srank;
-  a.by_srank = e.by_srank; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake; a.origin = e.origin;
+  a.by_srank = e.by_srank; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake; a.rinfo = e.rinfo; a.origin = e.origin;
   a.obkt = e.obkt; a.nfail = e.nfail; a.min_ingress = e.min_ingress; a.thr = e.thr; a.slot_prunes = e.slot_prunes;
   a.hops = e.hops; a.cnt = e.cnt; a.mask = e.mask; a.cmeta = e.cmeta; a.ckey = e.ckey;
   a.egress = e.egress; a.prune_round = e.prune_round; a.egress_acc = e.egress_acc; a.ingress_acc = e.ingress_acc;
