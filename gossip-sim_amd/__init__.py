@@ -28,6 +28,7 @@ GS_FLAG_NARROW_WAVE_PATH = 4
 GS_FLAG_BINNED_ALL_LEVELS = 8
 GS_FLAG_WIDE_RECORDS = 16
 GS_FLAG_NO_SMALL_LEVELS = 32
+GS_FLAG_MISPREDICT_LEVELS = 64
 HOP_UNREACHED = 0xFF
 B58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
 
@@ -190,7 +191,7 @@ class Engine:
     def __init__(self, stakes, n_slots, *, fanout=6, active_set_size=12, rotation_probability=0.013333, seed=0,
                  device=0, bfs_mode=GS_BFS_AUTO, inbound_capacity=0, profile=False, split_round=False,
                  narrow_wave_path=False, binned_all_levels=False, wide_records=False, no_small_levels=False,
-                 part=None):
+                 mispredict_levels=False, part=None):
         L = lib()
         self.stakes = np.ascontiguousarray(stakes, dtype=np.uint64)
         self.n = len(self.stakes)
@@ -200,7 +201,8 @@ class Engine:
                    (GS_FLAG_PROFILE if profile else 0) | (GS_FLAG_SPLIT_ROUND if split_round else 0) |
                    (GS_FLAG_NARROW_WAVE_PATH if narrow_wave_path else 0) |
                    (GS_FLAG_BINNED_ALL_LEVELS if binned_all_levels else 0) |
-                   (GS_FLAG_WIDE_RECORDS if wide_records else 0) | (GS_FLAG_NO_SMALL_LEVELS if no_small_levels else 0))
+                   (GS_FLAG_WIDE_RECORDS if wide_records else 0) | (GS_FLAG_NO_SMALL_LEVELS if no_small_levels else 0) |
+                   (GS_FLAG_MISPREDICT_LEVELS if mispredict_levels else 0))
         h = C.c_void_p()
         if part is None:
             _check(L.gs_create(C.byref(p), _ptr(self.stakes), self.n, n_slots, C.byref(h)))

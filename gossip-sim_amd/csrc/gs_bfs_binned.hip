@@ -252,6 +252,9 @@ __global__ __launch_bounds__(BIN_ST) void k_bin_small(BinArgs a, uint32_t mode, 
     if (mode == BIN_TAIL) {
       if (qn > 0) atomicOr(a.err, ERR_DEPTH);  // level 254 not empty
       const uint32_t nl = min(d, 255u);
+      // seqlock: 0 (in progress, the host skips it) before the sizes, the new seq after
+      __hip_atomic_store(&a.hprof[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __atomic_thread_fence(__ATOMIC_RELEASE);
       for (uint32_t k = 0; k < nl; ++k)
         __hip_atomic_store(&a.hprof[2 + k], __hip_atomic_load(&a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -352,7 +355,10 @@ __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply(BinArgs a, uint32_t
   const uint32_t qn = d < 254 ? a.lvl[d] : 0u;
   uint32_t* __restrict__ qnxt = (d & 1) ? qa : qb;
   if (qn == 0 || qn < a.qmin) return;  // (a direct level: no Lt entry, the gather skips it)
-  if (pi != BIN_NOPAIR && blockIdx.x == 0 && threadIdx.x == 0) a.dpair[pi + 1] = d + 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (pi != BIN_NOPAIR) a.dpair[pi + 1] = d + 1;
+    a.lvl[256 + d] = 1;  // level d's records are in Lt[d] (the gather reads them only then)
+  }
   const uint32_t b = xcd_bin(blockIdx.x, a.nbins);
   if (b >= a.nbins) return;
   const uint32_t tid = threadIdx.x, nb = a.nbins, BP = 1u << a.BS, NW = BP / 32;
@@ -471,7 +477,10 @@ __global__ __launch_bounds__(APPLY_THREADS) void k_bin_apply_sb(BinArgs a, uint3
   const uint32_t qn = d < 254 ? a.lvl[d] : 0u;
   uint32_t* __restrict__ qnxt = (d & 1) ? qa : qb;
   if (qn == 0 || qn < a.qmin) return;  // (a direct level: no Lt entry, the gather skips it)
-  if (pi != BIN_NOPAIR && blockIdx.x == 0 && threadIdx.x == 0) a.dpair[pi + 1] = d + 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (pi != BIN_NOPAIR) a.dpair[pi + 1] = d + 1;
+    a.lvl[256 + d] = 1;  // level d's records are in Lt[d] (the gather reads them only then)
+  }
   const uint32_t nb = a.nbins, nsb = (nb + SB_N - 1) >> SB_LOG;
   const uint32_t B = xcd_bin(blockIdx.x, nsb);
   if (B >= nsb) return;
@@ -603,8 +612,9 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_bin_gather(BinArgs a) {
   }
   uint32_t rn = 0;  // 1. run table: thread d < 255 reads level d's run
   if (tid < 255) {
-    const uint32_t q = a.lvl[tid];
-    if (q >= a.qmin && q) {
+    // Only levels an apply really ran: in the predicted loop a level the profile put below
+    // qmin runs direct whatever its real size, and its Lt row is stale.
+    if (a.lvl[256 + tid]) {
       const uint2 L = a.Lt[(size_t)tid * nb + b];
       rs[tid] = L.x;
       rn = L.y;
@@ -863,7 +873,8 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
       const uint32_t nl = std::min<uint32_t>((uint32_t)vp[1], 255u);
       std::vector<uint32_t> pv(nl);
       for (uint32_t k = 0; k < nl; ++k) pv[k] = vp[2 + k];
-      if (vp[0] == sq) {
+      std::atomic_thread_fence(std::memory_order_acquire);
+      if (vp[0] == sq) {  // (a rewrite sets 0 first, then a new seq)
         e.mv_pred[0] = std::move(pv);
         e.mv_prof_seen[0] = sq;
       }
@@ -879,8 +890,12 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
     const uint32_t npairs = std::min<uint32_t>(k1 - k0 + mv_margin(), 250);
     GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_small<A>), dim3(1), dim3(BIN_ST), 0, e.st, a, BIN_HEAD, 0u, 0u,
                                                 lim, e.q[0], e.q[1], e.mv_hstate_dev, 0u));
+    // GS_FLAG_MISPREDICT_LEVELS (tests): every other round inverts the predicted binned /
+    // direct choice of each pair, so real levels of >= qmin pairs run direct while the
+    // Lt rows of the round before are still there
+    const uint32_t flip = (e.prm.flags & GS_FLAG_MISPREDICT_LEVELS) ? (e.mv_seq & 1u) : 0u;
     for (uint32_t i = 0; i < npairs; ++i) {
-      const uint32_t binned = k0 + i < pv.size() && pv[k0 + i] >= a.qmin ? 1u : 0u;  // predicted binned level
+      const uint32_t binned = (k0 + i < pv.size() && pv[k0 + i] >= a.qmin ? 1u : 0u) ^ flip;  // predicted binned level
       GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_bin_expand<A, R>), dim3(xgrid), dim3(xth), lds_x, e.st, a, 0u, i,
                                                   binned, e.q[0], e.q[1]));
       if (binned) {
@@ -927,8 +942,9 @@ static hipError_t run_binned(Engine& e, BinArgs& a) {
       if (done) break;
     }
     if (!polled_only && lim > 0) {  // this round's sizes seed the prediction
-      std::vector<uint32_t> p2(nlev);
-      for (uint32_t k = 0; k < nlev; ++k) p2[k] = hl[k];
+      std::vector<uint32_t> p2(nlev);  // (levels past the BFS's end may still read PENDING: 0)
+      for (uint32_t k = 0; k < nlev; ++k) p2[k] = hl[k] == MV_PENDING ? 0u : hl[k];
+      while (!p2.empty() && p2.back() == 0) p2.pop_back();
       e.mv_pred[0] = std::move(p2);
     }
   }
@@ -951,7 +967,7 @@ hipError_t launch_bfs_binned(Engine& e, bool record) {
   a.PAIRS = e.PAIRS; a.pool_bin_cap = ((size_t)1 << e.bin.BS) * e.capin; a.record = record ? 1 : 0;
   hipError_t r;
   if ((r = hipMemsetAsync(e.hops, 0xFF, e.PAIRS, e.st)) != hipSuccess) return r;
-  if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st)) != hipSuccess) return r;
+  if ((r = hipMemsetAsync(e.lvl, 0, 512 * 4, e.st)) != hipSuccess) return r;  // sizes and binned flags
   if ((r = hipMemsetAsync(e.cnt, 0, e.PAIRS * 4, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.bin_binoff, 0, (size_t)e.bin.nbins * 4, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.bin_vis, 0, (e.PAIRS + 31) / 32 * 4, e.st)) != hipSuccess) return r;

@@ -629,6 +629,9 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
     if (mode == MV_TAIL) {  // the round's level profile for the host's next prediction
       uint32_t* hp = a.hprof;
       const uint32_t nl = min(d, 255u);
+      // seqlock: 0 (in progress, the host skips it) before the sizes, the new seq after
+      __hip_atomic_store(&hp[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __atomic_thread_fence(__ATOMIC_RELEASE);  // (the 0 is visible before any size)
       for (uint32_t k = 0; k < nl; ++k) __hip_atomic_store(&hp[2 + k], a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&hp[1], nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&hp[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1335,7 +1338,8 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
         const uint32_t nl = std::min<uint32_t>((uint32_t)vp[1], 255u);
         std::vector<uint32_t> pv(nl);
         for (uint32_t k = 0; k < nl; ++k) pv[k] = vp[2 + k];
-        if (vp[0] == sq) {  // (not rewritten meanwhile)
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (vp[0] == sq) {  // (not rewritten meanwhile: a rewrite sets 0 first, then a new seq)
           e.mv_pred[g] = std::move(pv);
           e.mv_prof_seen[g] = sq;
         }
@@ -1349,8 +1353,13 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     if (pv.empty() || polled_only || e.mv_diag) {
       if ((r = mv_group_polled(e, a, gr, lag, nlev))) return r;
       if (!polled_only) {  // this round's sizes seed the prediction
+        // (levels enqueued after the one that ended the BFS may not have run yet: PENDING = 0)
         std::vector<uint32_t> p2(nlev);
-        for (uint32_t k = 0; k < nlev; ++k) p2[k] = e.mv_hlvl[k];
+        for (uint32_t k = 0; k < nlev; ++k) {
+          const uint32_t x = e.mv_hlvl[k];
+          p2[k] = x == MV_PENDING ? 0u : x;
+        }
+        while (!p2.empty() && p2.back() == 0) p2.pop_back();
         e.mv_pred[g] = std::move(p2);
       }
     } else {

@@ -372,7 +372,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     ALLOC(e->mv_seed, S, 0);
   }
   e->h_nfail_any.assign(S, 0);
-  ALLOC(e->lvl, 256, 0);
+  ALLOC(e->lvl, 512, 0);  // [256] level sizes; binned BFS: [256 + d] = 1 iff level d was binned this round
   ALLOC(e->rot_list, N, 0);
   ALLOC(e->rot_count, 2, 0);
   ALLOC(e->rot_changed, N * NB, 0);

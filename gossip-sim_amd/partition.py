@@ -67,7 +67,12 @@ class PartitionedEngine:
         if exchange not in ("auto", "records", "dense"):
             raise ValueError("exchange must be auto, records or dense")
         self.exchange = exchange
-        self.dense = None      # [N * S] int32 exchange buffer, allocated on the first dense round
+        # [N * S] int32 dense exchange buffer (4 * S * N bytes: 640 MB at C5's 10M x 16),
+        # allocated here -- not in the round that first goes dense, where a failed allocation
+        # on one rank would leave the others waiting in the all-reduce
+        self.dense = None
+        if exchange != "records":
+            self.dense = torch.zeros(self.dense_words, dtype=torch.int32, device=self.dev)
         self.records = 0       # prune records of the last round (all ranks)
         self.last_mode = None  # "records" / "dense" / None (no prunes)
         self.bytes_in = 0      # exchange bytes this rank received over all rounds (collective payload)
@@ -105,8 +110,6 @@ class PartitionedEngine:
                 raise RuntimeError(f"{m} prune records exceed the record buffer ({self.record_cap}); "
                                    "use exchange='auto' or 'dense'")
             if dense:
-                if self.dense is None:
-                    self.dense = torch.zeros(self.dense_words, dtype=torch.int32, device=self.dev)
                 _check(L.gs_part_prunes_dense_out(h, self._ptr(self.dense), dev))
                 tdist.all_reduce(self.dense, group=self.group)
                 self._done()

@@ -57,7 +57,7 @@ enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24
  * else LEVEL. */
 enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2, GS_BFS_BINNED = 3, GS_BFS_MULTI = 4 };
 enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4, GS_FLAG_BINNED_ALL_LEVELS = 8,
-       GS_FLAG_WIDE_RECORDS = 16, GS_FLAG_NO_SMALL_LEVELS = 32 };
+       GS_FLAG_WIDE_RECORDS = 16, GS_FLAG_NO_SMALL_LEVELS = 32, GS_FLAG_MISPREDICT_LEVELS = 64 };
 
 typedef struct gs_params {
   uint32_t push_fanout;         /* Config::gossip_push_fanout (gossip.rs:113) */
@@ -82,7 +82,10 @@ typedef struct gs_params {
                                    even where 4-byte ones fit (same results);
                                    GS_FLAG_NO_SMALL_LEVELS: GS_BFS_BINNED / GS_BFS_MULTI run no level
                                    in their single-workgroup small-level kernels (every level
-                                   through the grid-wide kernels; same results) */
+                                   through the grid-wide kernels; same results);
+                                   GS_FLAG_MISPREDICT_LEVELS: GS_BFS_BINNED's predicted level loop
+                                   inverts its binned/direct choice per level every other round
+                                   (same results; a test of the misprediction path) */
 } gs_params;
 
 typedef struct gs_slot {

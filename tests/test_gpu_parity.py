@@ -421,22 +421,27 @@ def test_large_network_invariants():
         assert (dest >= 0).all()
 
 
-@pytest.mark.parametrize("all_levels,wide", [(False, False), (True, False), (True, True)])
-def test_binned_bfs_matches_level_bfs_large(all_levels, wide):
+@pytest.mark.parametrize("all_levels,wide,mispredict", [(False, False, False), (True, False, False),
+                                                        (True, True, False), (False, False, True),
+                                                        (True, False, True)])
+def test_binned_bfs_matches_level_bfs_large(all_levels, wide, mispredict):
     """N = 300k, 3 slots, a fail-nodes fraction: the propagation-blocked BFS (hybrid
     with the direct kernel for small levels, or binned throughout; 4- or 8-byte
     records) gives the level BFS's hops, in-degrees, inbound sets, counters and
-    summaries."""
+    summaries. `mispredict`: the predicted level loop inverts its binned/direct choice
+    every other round, so levels of >= 2^17 pairs run direct while the previous round's
+    pool runs (Lt) are still in memory -- the gather must take only this round's binned
+    levels."""
     n = 300_000
     st = eb.synth.power_law_stakes(n)
     engs = [gs.Engine(st, 3, seed=33, rotation_probability=0.01, bfs_mode=gs.GS_BFS_LEVEL),
             gs.Engine(st, 3, seed=33, rotation_probability=0.01, bfs_mode=gs.GS_BFS_BINNED,
-                      binned_all_levels=all_levels, wide_records=wide)]
+                      binned_all_levels=all_levels, wide_records=wide, mispredict_levels=mispredict)]
     for e in engs:
         e.set_slots([0, 17, n - 1], [2, 1, 3], [0.15, 0.3, 0.05])
         e.init_active_sets()
         e.fail_nodes([0.0, 0.2, 0.1])
-    for r in range(4):
+    for r in range(6 if mispredict else 4):
         for e in engs:
             e.round(r, record=r >= 1)
         a, b = engs
