@@ -64,25 +64,60 @@ def load_pkg():
     return mod
 
 
+_KHASH = None
+
+
+def kernel_hash():
+    global _KHASH
+    if _KHASH is None:
+        _KHASH = sys.modules["gossip_sim_amd"].kernel_hash() if "gossip_sim_amd" in sys.modules \
+            else load_pkg().kernel_hash()
+    return _KHASH
+
+
 def pmc_traffic(tag):
     """HBM bytes per launch from the newest committed rocprofv3 --pmc summary named
-    profiles/r*/pmc_<tag>.json (scripts/pmc.sh + scripts/pmc_summary.py), or None."""
+    profiles/r*/pmc_<tag>.json (scripts/pmc_summary.py, scripts/pmc_round.py), or None.
+    A summary counts only if it is stamped with the kernel hash of the sources the library
+    is built from (gossip_sim_amd.kernel_hash): a profile of other kernels gives null and
+    the reason. Returns (bytes, source, note)."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{tag}.json")), reverse=True):
         with open(path) as f:
             d = json.load(f)
-        return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
-    return None, None
+        src = os.path.relpath(path, ROOT)
+        kh = d.get("kernel_hash")
+        if kh != kernel_hash():
+            return None, src, f"stale: {src} measured kernels {kh}, built kernels are {kernel_hash()}"
+        return d["traffic_bytes_per_launch"], src, f"PMC at kernel hash {kh}"
+    return None, None, "no PMC summary for this window"
+
+
+def trace_window(tag):
+    """The committed rocprofv3 kernel-trace average of the same window
+    (profiles/r*/trace_<tag>.json, scripts/trace_window.py), if stamped with the built
+    kernels' hash: (avg_us, source) or (None, reason)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"trace_{tag}.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        src = os.path.relpath(path, ROOT)
+        if d.get("kernel_hash") != kernel_hash():
+            return None, f"stale: {src} traced kernels {d.get('kernel_hash')}"
+        return round(d["avg_us"], 2), src
+    return None, "no kernel trace of this window"
 
 
 def roofline(bytes_total, ms, launches, kernel, model, traffic_tag=None):
     if ms <= 0:
         return None
     ach = bytes_total / (ms * 1e-3) / 1e9
-    traffic, tsrc = pmc_traffic(traffic_tag) if traffic_tag else (None, None)
+    traffic, tsrc, tnote = pmc_traffic(traffic_tag) if traffic_tag else (None, None, "not collected")
+    tr_us, tr_src = trace_window(traffic_tag) if traffic_tag else (None, "not collected")
     return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc, "kernel": kernel,
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+            "traffic_note": tnote, "kernel_hash": kernel_hash(), "kernel": kernel,
             "bytes_model": model, "bytes_per_launch": round(bytes_total / max(launches, 1)),
-            "avg_launch_us": round(ms * 1e3 / max(launches, 1), 2), "launches": launches}
+            "avg_launch_us": round(ms * 1e3 / max(launches, 1), 2), "launches": launches,
+            "rocprof_avg_us": tr_us, "rocprof_source": tr_src}
 
 
 def b_prop(V, E, asz):

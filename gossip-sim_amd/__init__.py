@@ -136,6 +136,21 @@ EXPORTS = {
 _lib = None
 
 
+def kernel_hash():
+    """sha256 (16 hex digits) of the device sources libgossip_hip.so is built from
+    (csrc/*.hip, csrc/*.h). Profiles under profiles/ carry the hash of the kernels they
+    measured; bench.py reports a profile's figures only when it equals this one."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(PKG_DIR, "csrc")
+    for name in sorted(os.listdir(d)):
+        if name.endswith((".hip", ".h")):
+            h.update(name.encode() + b"\0")
+            with open(os.path.join(d, name), "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def build(quiet=True):
     """Compile libgossip_hip.so (and the gossip-sim CLI) for gfx950 in-tree."""
     cmd = ["make", "-C", PKG_DIR, "-j8"]

@@ -22,10 +22,10 @@
 //   apply (one workgroup per coarse bin, bins dealt to XCDs in contiguous ranges): ORs
 //     the level's records into an LDS copy of the bin's vis masks -- new bits are first
 //     arrivals at hop d+1 (gossip.rs:594-600) -- appends new nodes to the next frontier
-//     (one entry per distinct entry k) and the level's records to the bin's pool run.
+//     (one entry per distinct entry k) and the level's records, stamped with their hop,
+//     to the fine bins' pools.
 //   gather (after the last level, one workgroup per fine bin of 2^BSF nodes): the
-//     fine bin's records of every level (its coarse bin's pool runs, filtered) as an LDS
-//     CSR by destination; per (slot, node): in-degree, the inbound records
+//     fine bin's pool (records of every level) as an LDS CSR by destination; per (slot, node): in-degree, the inbound records
 //     hop << 24 | src (gossip.rs:601-607) as rows inb[c][pair] coalesced over nodes, and
 //     the hop (1 + the smallest pusher level; 0 at the origin; unreached = 0xFF).
 //
@@ -73,14 +73,12 @@ struct MvArgs {
   uint32_t* lvl;          // [256] frontier entries per level
   uint32_t* hlvl;         // host-mapped [256]: expand(d) writes lvl[d] here (the polled loop)
   uint32_t* dpair;        // [258] level of expand/apply pair i (predicted loop): head writes [0], apply(i) [i + 1]
-  uint32_t* snapg;        // [fno] small-level kernel: level-start pool fills when they do not fit LDS
   uint32_t* hprof;        // host-mapped: the tail kernel's level profile (seq, levels, sizes)
   uint32_t* T;            // [rows_cap][TW] rows of the current level
   unsigned long long* area;  // records of the current level
   uint32_t* ctr;          // [0] records used in area (this level)
-  unsigned long long* pool;  // [fno][pcap] records of the round, per (kept) fine bin, level runs
+  unsigned long long* pool;  // [fno][pcap] records of the round per (kept) fine bin (mv_pool_rec)
   uint32_t* pused;        // [fno] records in each fine bin's pool region
-  uint2* Lt;              // [256][fno] (pool start, count) of fine bin flo + i at level d
   uint32_t* cmeta;        // fused consume (gs_round): the received caches, as in gs_consume_g.hip
   uint32_t* ckey;
   uint8_t* prune_round;
@@ -97,6 +95,14 @@ struct MvArgs {
   uint32_t small;  // levels of at most this many entries run in the one-workgroup kernel
   size_t PAIRS, area_cap, rows_cap, q_cap, pcap;
 };
+
+// A pool record: src | node-in-fine-bin << UB | hop << (UB + BSF) | slot mask << (UB + BSF + 8)
+// (mv_geometry keeps UB + BSF + 8 + GW <= 64). The hop travels with the record, so the
+// gather reads a fine bin's pool as one run whatever the level each record came from.
+__device__ inline unsigned long long mv_pool_rec(const MvArgs& a, uint32_t u, uint32_t vf, uint32_t hop, uint32_t m) {
+  return (unsigned long long)u | ((unsigned long long)vf << a.UB) | ((unsigned long long)hop << (a.UB + a.BSF)) |
+         ((unsigned long long)m << (a.UB + a.BSF + 8));
+}
 
 __device__ inline uint32_t mv_xcd_bin(uint32_t i, uint32_t nbins) {
   const uint32_t per = (nbins + 7) / 8;
@@ -403,19 +409,20 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
       if (fb != 0xFFFFu) {
         const uint32_t fl = f0 + fb - a.flo;
         const size_t pp = (size_t)a.pused[fl] + pos;
-        if (pp < a.pcap) a.pool[(size_t)fl * a.pcap + pp] = rec;
+        if (pp < a.pcap)
+          a.pool[(size_t)fl * a.pcap + pp] = mv_pool_rec(a, (uint32_t)rec & ((1u << UB) - 1), vl & ((1u << a.BSF) - 1),
+                                                         d + 1, (uint32_t)(rec >> (UB + BSC)));
       }
     }
     __syncthreads();
   }
   __syncthreads();
-  if (tid < NF && f0 + tid - a.flo < a.fno) {  // the level's run of each kept fine bin, for the gather
+  if (tid < NF && f0 + tid - a.flo < a.fno) {  // each kept fine bin's pool fill
     const uint32_t fl = f0 + tid - a.flo;
     const uint32_t used = a.pused[fl], n = fcur[tid];
     const bool over = (size_t)used + n > a.pcap;
     if (over) atomicOr(a.err, ERR_MV_CAP);
-    a.Lt[(size_t)d * a.fno + fl] = make_uint2(used, over ? 0u : n);
-    a.pused[fl] = over ? used : used + n;
+    if (n) a.pused[fl] = over ? (uint32_t)a.pcap : used + n;
   }
   if (!loaded) return;  // no records: no first arrivals in this bin
   // first arrivals (hop d + 1) become next-level entries, in node order
@@ -486,16 +493,13 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
                                                     uint2* __restrict__ q0, uint2* __restrict__ q1,
                                                     uint32_t* __restrict__ hstate, const uint2* __restrict__ seeds,
                                                     uint32_t nseed, uint32_t seq) {
-  // [fno] pool fill at level start, then (when LP) [fno] the running fill: the records'
-  // pool places come from LDS atomics, the global fills are written once at the end
-  extern __shared__ __attribute__((aligned(16))) uint32_t snap_l[];
+  // (when LP) [fno] the pool fills: the records' pool places come from LDS atomics, the
+  // global fills are written once at the end
+  extern __shared__ __attribute__((aligned(16))) uint32_t lp[];
   __shared__ uint2 qL[2][MV_SQ];
   __shared__ uint32_t sorg[32], sfk[32], gt[GT_WORDS], cnt_s;
-  const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BPm = (1u << BSC) - 1;
-  const bool LP = a.fno <= MV_SMALL_LP;  // (uniform)
-  // (beyond MV_SMALL_LP fine bins the level-start fills live in global memory: a.snapg)
-  uint32_t* snap = LP ? snap_l : a.snapg;
-  uint32_t* lp = snap_l + a.fno;
+  const uint32_t tid = threadIdx.x;
+  const bool LP = a.fno <= MV_SMALL_LP;  // (uniform; beyond, device-scope atomics on a.pused)
   if (tid < a.Sg) {
     sorg[tid] = a.origin[a.s0 + tid];
     sfk[tid] = a.fk[a.s0 + tid];
@@ -507,7 +511,6 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
     for (uint32_t i = tid; i < 256; i += MV_ST) a.lvl[i] = i == 0 ? nseed : 0u;
     for (uint32_t f = tid; f < a.fno; f += MV_ST) {
       a.pused[f] = 0;
-      snap[f] = 0;
       if (LP) lp[f] = 0;
     }
     if (tid == 0) a.ctr[0] = 0;
@@ -518,11 +521,8 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
     }
     inL = true;
     __syncthreads();  // (full: the seeds' vis stores land before any vis atomic)
-  } else {
-    for (uint32_t f = tid; f < a.fno; f += MV_ST) {
-      snap[f] = mv_ld(&a.pused[f]);
-      if (LP) lp[f] = snap[f];
-    }
+  } else if (LP) {
+    for (uint32_t f = tid; f < a.fno; f += MV_ST) lp[f] = mv_ld(&a.pused[f]);
   }
   // GS_PHASE_PROFILE: section clocks of thread 0 at pclk[0..4] (setup, expand loads,
   // atomics + places, Lt + barrier; [4] levels)
@@ -583,8 +583,7 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
         if (pp[s] != 0xFFFFFFFFu) {
           const uint32_t f = (w >> a.BSF) - a.flo;
           if (pp[s] < a.pcap)
-            a.pool[(size_t)f * a.pcap + pp[s]] = (unsigned long long)u | ((unsigned long long)(w & BPm) << UB) |
-                                                 ((unsigned long long)acc[s] << (UB + BSC));
+            a.pool[(size_t)f * a.pcap + pp[s]] = mv_pool_rec(a, u, w & ((1u << a.BSF) - 1), d + 1, acc[s]);
           else
             atomicOr(a.err, ERR_MV_CAP);
         }
@@ -604,11 +603,6 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
     }
     lds_barrier();
     mark(2);
-    for (uint32_t f = tid; f < a.fno; f += MV_ST) {  // the level's pool run of every kept fine bin
-      const uint32_t now = LP ? lp[f] : mv_ld(&a.pused[f]);
-      a.Lt[(size_t)d * a.fno + f] = make_uint2(snap[f], now - snap[f]);
-      snap[f] = now;
-    }
     qn = min(cnt_s, (uint32_t)a.q_cap);
     ++d;
     if (tid == 0) a.lvl[d] = qn;
@@ -618,7 +612,7 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
     mark(3);
   }
   if (LP)
-    for (uint32_t f = tid; f < a.fno; f += MV_ST) a.pused[f] = lp[f];
+    for (uint32_t f = tid; f < a.fno; f += MV_ST) a.pused[f] = min(lp[f], (uint32_t)a.pcap);
   if (qn > 0 && inL && mode != MV_TAIL) {  // the next level's entries for expand: the LDS part to global memory
     uint2* qg = (d & 1) ? q1 : q0;
     for (uint32_t i = tid; i < min(qn, MV_SQ); i += MV_ST) qg[i] = qL[d & 1][i];
@@ -658,24 +652,24 @@ constexpr uint32_t MV_WSCR = 64 + CACHE_CAP;  // fused consume: per-wave LDS scr
 constexpr uint32_t MV_CSCR = (MV_GT / 64) * MV_WSCR * 4;  // bytes of all waves' scratch
 
 __host__ __device__ inline size_t mv_gather_fixed_bytes(uint32_t BSF) {
-  return 4 * (256 + 257 + 2 * (((size_t)1 << BSF) + 1) + 16 + 32);
+  return 4 * (2 * (((size_t)1 << BSF) + 1) + 16 + 32);
 }
 
 // The LDS CSR of one fine bin's records: cn[i] .. cn[i + 1] (minus the range base) index
 // node i's records keys[] = hop << 24 | src and msk[] = slot masks.
 struct MvCsr {
-  uint32_t *rs, *rp, *cn, *cur, *ctl, *sorg, *keys, *msk;
+  uint32_t *cn, *cur, *ctl, *sorg, *keys, *msk;
 };
 
-// After the last level, per kept fine bin f (local index; node base v0): the bin's records of every level (its pool runs,
-// in level order) as an LDS CSR by destination. Nodes whose records exceed gcap are
-// taken in consecutive ranges; body(lo, hi, base) runs on each range (all threads; no
-// barrier inside body is needed, one follows it).
+// After the last level, per kept fine bin f (local index; node base v0): the bin's pool
+// (records of every level, mv_pool_rec) as an LDS CSR by destination. Nodes whose records
+// exceed gcap are taken in consecutive ranges; body(lo, hi, base) runs on each range (all
+// threads; no barrier inside body is needed, one follows it).
 template <class Body>
-__device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, uint32_t nv, uint32_t gcap,
-                                  const MvCsr& L, Body body) {
-  const uint32_t tid = threadIdx.x, UB = a.UB, BSC = a.BSC, BSF = a.BSF, BP = 1u << BSF, BPm = BP - 1;
-  const uint32_t um = (1u << UB) - 1;
+__device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nv, uint32_t gcap, const MvCsr& L,
+                                  Body body) {
+  const uint32_t tid = threadIdx.x, UB = a.UB, BSF = a.BSF, BP = 1u << BSF, BPm = BP - 1;
+  const uint32_t um = (1u << UB) - 1, MS = UB + BSF + 8;
   unsigned long long tm = a.pclk && tid == 0 ? wall_clock64() : 0;
   auto mark = [&](int ph) {
     if (a.pclk && tid == 0) {
@@ -684,52 +678,32 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, ui
       tm = now;
     }
   };
-  uint32_t *rs = L.rs, *rp = L.rp, *cn = L.cn, *cur = L.cur, *ctl = L.ctl, *keys = L.keys, *msk = L.msk;
+  uint32_t *cn = L.cn, *cur = L.cur, *ctl = L.ctl, *keys = L.keys, *msk = L.msk;
   const unsigned long long* pool = a.pool + (size_t)f * a.pcap;  // (f: local kept-bin index)
   for (uint32_t i = tid; i <= BP; i += MV_GT) cn[i] = 0;
   if (tid < a.Sg) L.sorg[tid] = a.origin[a.s0 + tid];
-  {  // the run table: thread d reads level d's (start, count); exclusive prefix of the counts
-    uint32_t n = 0;
-    if (tid < 256) {
-      rs[tid] = 0;
-      if (tid < nlev && a.lvl[tid]) {  // an empty level wrote no run
-        const uint2 R = a.Lt[(size_t)tid * a.fno + f];
-        rs[tid] = R.x;
-        n = R.y;
-      }
-    }
-    const uint32_t incl = wave_incl_scan(n);
-    if ((tid & 63) == 63) ctl[tid >> 6] = incl;
-    __syncthreads();
-    uint32_t off = incl - n;
-    for (uint32_t w = 0; w < (tid >> 6); ++w) off += ctl[w];
-    if (tid < 256) rp[tid] = off;
-    if (tid == 255) rp[256] = off + n;
-  }
+  const uint32_t Etot = min(a.pused[f], (uint32_t)a.pcap);
+  auto key_of = [&](unsigned long long rec) {
+    return (((uint32_t)(rec >> (UB + BSF)) & 0xFFu) << 24) | ((uint32_t)rec & um);
+  };
   __syncthreads();
-  const uint32_t Etot = rp[256];
   // 1. count per node; the first MV_GC records of each thread stay in registers (key, mask, node)
   uint32_t kc[MV_GC], mc[MV_GC], vc[MV_GC];
-  uint32_t lv = 0;
 #pragma unroll
   for (uint32_t j = 0; j < MV_GC; ++j) {
     const uint32_t t = tid + j * MV_GT;
     kc[j] = 0; mc[j] = 0; vc[j] = 0xFFFFFFFFu;
     if (t < Etot) {
-      while (t >= rp[lv + 1]) ++lv;
-      const unsigned long long rec = pool[rs[lv] + (t - rp[lv])];
-      kc[j] = ((lv + 1) << 24) | ((uint32_t)rec & um);
-      mc[j] = (uint32_t)(rec >> (UB + BSC));
+      const unsigned long long rec = pool[t];
+      kc[j] = key_of(rec);
+      mc[j] = (uint32_t)(rec >> MS);
       vc[j] = (uint32_t)(rec >> UB) & BPm;
     }
   }
 #pragma unroll
   for (uint32_t j = 0; j < MV_GC; ++j)
     if (vc[j] != 0xFFFFFFFFu) atomicAdd(&cn[vc[j]], 1u);
-  for (uint32_t t = tid + MV_GC * MV_GT; t < Etot; t += MV_GT) {
-    while (t >= rp[lv + 1]) ++lv;
-    atomicAdd(&cn[(uint32_t)(pool[rs[lv] + (t - rp[lv])] >> UB) & BPm], 1u);
-  }
+  for (uint32_t t = tid + MV_GC * MV_GT; t < Etot; t += MV_GT) atomicAdd(&cn[(uint32_t)(pool[t] >> UB) & BPm], 1u);
   __syncthreads();
   mark(12);
   const uint32_t E2 = mv_block_scan(cn, BP, ctl);
@@ -761,16 +735,14 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, ui
     return hi;
   };
   auto place_pool = [&](uint32_t lo, uint32_t hi, uint32_t t0) {
-    uint32_t lp = 0;
     for (uint32_t t = tid + t0; t < Etot; t += MV_GT) {
-      while (t >= rp[lp + 1]) ++lp;
-      const unsigned long long rec = pool[rs[lp] + (t - rp[lp])];
+      const unsigned long long rec = pool[t];
       const uint32_t vl = (uint32_t)(rec >> UB) & BPm;
       if (vl < lo || vl >= hi) continue;
       const uint32_t p = atomicAdd(&cur[vl], 1u);
       if (p < gcap) {
-        keys[p] = ((lp + 1) << 24) | ((uint32_t)rec & um);
-        msk[p] = (uint32_t)(rec >> (UB + BSC));
+        keys[p] = key_of(rec);
+        msk[p] = (uint32_t)(rec >> MS);
       }
     }
     __syncthreads();
@@ -798,9 +770,7 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nlev, ui
 
 __device__ inline MvCsr mv_csr_lds(unsigned char* smem, uint32_t BP, uint32_t gcap) {
   MvCsr L;
-  L.rs = reinterpret_cast<uint32_t*>(smem);  // [256] pool start of level d's run
-  L.rp = L.rs + 256;                         // [257] records before level d's run
-  L.cn = L.rp + 257;                         // [BP + 1] records per node -> CSR starts
+  L.cn = reinterpret_cast<uint32_t*>(smem);  // [BP + 1] records per node -> CSR starts
   L.cur = L.cn + BP + 1;                     // [BP + 1] placement cursors
   L.ctl = L.cur + BP + 1;                    // [16]
   L.sorg = L.ctl + 16;                       // [32]
@@ -872,7 +842,7 @@ __device__ inline uint32_t mv_pair_hop(const MvCsr& L, uint32_t r0, uint32_t r1,
 // A node with more than MV_GH records (all slots) is deferred to a whole wave: stake
 // weights make in-degrees power-law, and one such node in a wave of lanes held the
 // other 63 lanes for its whole list (every slot). (256; 4 under GS_FLAG_NARROW_WAVE_PATH)
-__global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
+__global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t f = mv_xcd_bin(blockIdx.x, a.fno);  // local kept-bin index
   if (f >= a.fno) return;
@@ -881,7 +851,7 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a, uint32_t nlev) {
   const uint32_t nv = min(BP, a.vhi - v0), gcap = a.gcap;
   const MvCsr L = mv_csr_lds(smem, BP, gcap);
   bool over = false;
-  mv_bin_csr(a, f, nlev, nv, gcap, L, [&](uint32_t lo, uint32_t hi, uint32_t base) {
+  mv_bin_csr(a, f, nv, gcap, L, [&](uint32_t lo, uint32_t hi, uint32_t base) {
     const unsigned long long tb = a.pclk && tid == 0 ? wall_clock64() : 0;
     uint32_t* hvl = L.cur;  // the placement cursors are dead here: the heavy-node list
     for (uint32_t i = lo + tid; i < hi; i += MV_GT) {
@@ -961,7 +931,7 @@ __device__ inline void mv_after_consume(const MvArgs& a, uint32_t q, uint32_t me
 // of gs_consume_dev.h; in-degree and hop as in k_mv_gather. Lanes walk nodes, so the
 // cache rows stay coalesced. Pairs with in-degree > lane_c are taken by the whole wave
 // (records compacted by ballot, sorted across lanes), > wave_c by one lane.
-__global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void k_mv_consume(MvArgs a, uint32_t nlev) {
+__global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void k_mv_consume(MvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t f = mv_xcd_bin(blockIdx.x, a.fno);  // local kept-bin index
   if (f >= a.fno) return;
@@ -972,7 +942,7 @@ __global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void
   const MvCsr L = mv_csr_lds(smem + MV_CSCR, BP, gcap);
   const size_t PAIRS = a.PAIRS;
   uint32_t over = 0, errf = 0;
-  mv_bin_csr(a, f, nlev, nv, gcap, L, [&](uint32_t lo, uint32_t hi, uint32_t base) {
+  mv_bin_csr(a, f, nv, gcap, L, [&](uint32_t lo, uint32_t hi, uint32_t base) {
     for (uint32_t i0 = lo; i0 < hi; i0 += MV_GT) {  // block-uniform trip count
       const uint32_t i = i0 + tid;
       const bool in = i < hi;
@@ -1085,7 +1055,9 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   g.BSF = std::max(g.BSF, g.BSC > 4 ? g.BSC - 4 : 0u);
   g.nbc = (N + (1u << g.BSC) - 1) >> g.BSC;
   g.nbf = g.nbc << (g.BSC - g.BSF);
-  g.GW = std::min(28u, (64u - g.UB - g.BSC) & ~3u);
+  // slot masks: area records (src | node-in-coarse-bin | mask) and pool records (src |
+  // node-in-fine-bin | hop | mask, mv_pool_rec) are 64 bits
+  g.GW = std::min(28u, std::min((64u - g.UB - g.BSC) & ~3u, (64u - g.UB - g.BSF - 8) & ~3u));
   g.TW = g.nbc + 2;
   const size_t sg = std::min<size_t>(S, g.GW);
   g.q_cap = (size_t)N * std::min<size_t>(sg, 26) + 64;
@@ -1170,8 +1142,8 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.origin = e.origin; a.mask = e.mask; a.gt = e.mv_gtab + (size_t)g * GT_WORDS;
   a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb; a.egress = e.egress; a.err = e.err;
   a.vis = e.mv_vis; a.lvl = e.lvl; a.hlvl = e.mv_hlvl_dev; a.T = e.mv_T; a.area = e.mv_area; a.ctr = e.mv_ctr;
-  a.dpair = e.mv_dpair; a.hprof = nullptr; a.snapg = e.mv_snapg;
-  a.pool = e.mv_pool; a.pused = e.mv_pused; a.Lt = e.mv_Lt;
+  a.dpair = e.mv_dpair; a.hprof = nullptr;
+  a.pool = e.mv_pool; a.pused = e.mv_pused;
   a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
   a.vlo = e.vlo; a.vhi = e.vlo + e.NP; a.NP = e.NP; a.MSU = (uint32_t)e.msu;
@@ -1248,7 +1220,7 @@ static hipError_t mv_group_polled(Engine& e, MvArgs& a, const MvGroup& gr, uint3
   const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)MV_XT * e.ASZP * 8;
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
   const uint32_t fno = mv_kept_bins(e);
-  const size_t lds_s = fno <= MV_SMALL_LP ? (size_t)fno * 8 : 0;
+  const size_t lds_s = fno <= MV_SMALL_LP ? (size_t)fno * 4 : 0;
   const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8, xgrid = 2048;
   volatile uint32_t* hl = e.mv_hlvl;        // host-mapped: expand(d) writes lvl[d]
   volatile uint32_t* hs = e.mv_hlvl + 256;  // host-mapped: the small-level kernel's (level, entries)
@@ -1296,7 +1268,7 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
   const size_t lds_g = mv_glds();
   const uint32_t fno = mv_kept_bins(e);
-  const size_t lds_s = fno <= MV_SMALL_LP ? (size_t)fno * 8 : 0;
+  const size_t lds_s = fno <= MV_SMALL_LP ? (size_t)fno * 4 : 0;
   if (!e.mv_attr_set) {
     GS_ASZP_DISPATCH(e.ASZP, {
       r = hipFuncSetAttribute((const void*)k_mv_expand<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
@@ -1384,8 +1356,8 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     }
     e.tend("bfs", t0);
     e.tbegin(consume ? "gather_consume" : "gather", &t0);
-    if (consume) hipLaunchKernelGGL(k_mv_consume, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a, nlev);
-    else hipLaunchKernelGGL(k_mv_gather, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a, nlev);
+    if (consume) hipLaunchKernelGGL(k_mv_consume, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a);
+    else hipLaunchKernelGGL(k_mv_gather, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a);
     e.tend(consume ? "gather_consume" : "gather", t0);
     if (e.mv_diag) {  // GS_MV_DIAG=1: entries and records of the group's BFS (diagnostics)
       std::vector<uint32_t> pu(fno);
@@ -1397,14 +1369,8 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       for (uint32_t x : pu) { rec += x; mx = std::max<size_t>(mx, x); }
       std::fprintf(stderr, "GS_MV_DIAG group %u: levels %u, entries %zu, records %zu (max %zu per fine bin)\n", g,
                    nlev, ent, rec, mx);
-      std::vector<uint2> lt((size_t)nlev * fno);
-      if ((r = hipMemcpy(lt.data(), e.mv_Lt, lt.size() * sizeof(uint2), hipMemcpyDeviceToHost))) return r;
-      std::fprintf(stderr, "GS_MV_DIAG levels (entries/records):");
-      for (uint32_t d = 0; d < nlev; ++d) {
-        size_t rd = 0;
-        for (uint32_t f = 0; f < fno; ++f) rd += lt[(size_t)d * fno + f].y;
-        std::fprintf(stderr, " %u/%zu", hl[d], rd);
-      }
+      std::fprintf(stderr, "GS_MV_DIAG levels (entries):");
+      for (uint32_t d = 0; d < nlev; ++d) std::fprintf(stderr, " %u", hl[d]);
       std::fprintf(stderr, "\n");
     }
   }

@@ -362,8 +362,6 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     b0 = e->dev_bytes;
     ALLOC(e->mv_pool, (size_t)fno * g.pcap, 0);
     ALLOC(e->mv_pused, fno, 0);
-    ALLOC(e->mv_snapg, fno, 0);
-    ALLOC(e->mv_Lt, (size_t)256 * fno, 0);
     e->pair_bytes += e->dev_bytes - b0;
     ALLOC(e->mv_fcls, N, 0xFF);
     ALLOC(e->mv_fk, S, 0);

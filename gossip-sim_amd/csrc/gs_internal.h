@@ -31,7 +31,8 @@ struct BinGeom {
 };
 
 // Geometry of the multi-source frontier BFS (gs_bfs_multi.hip): bins of 2^BS nodes,
-// records u64 = src | node-in-bin << UB | slot mask << (UB + BS), slot groups of <= GW.
+// level records u64 = src | node-in-coarse-bin << UB | slot mask << (UB + BSC); pool records
+// src | node-in-fine-bin << UB | hop << (UB + BSF) | slot mask << (UB + BSF + 8); slot groups of <= GW.
 constexpr uint32_t GT_WORDS = 96;  // per-group table words
 struct MvGeom {
   uint32_t UB = 0, BSC = 0, BSF = 0, nbc = 0, nbf = 0, GW = 0, TW = 0, gcap = 0, gcap_c = 0;
@@ -116,7 +117,6 @@ struct Engine {
   uint32_t* mv_ctr = nullptr;     // [4] records used
   unsigned long long* mv_pool = nullptr;  // [nbf][pcap] records of the round per fine bin
   uint32_t* mv_pused = nullptr;   // [nbf]
-  uint2* mv_Lt = nullptr;         // [256][nbf] (pool start, count) per level and fine bin
   uint8_t* mv_fcls = nullptr;     // [N] failure class per node
   uint8_t* mv_fk = nullptr;       // [S] failure class index per slot
   uint32_t* mv_thr = nullptr;     // [S] distinct failure counts (scratch)
@@ -124,7 +124,6 @@ struct Engine {
   uint32_t* mv_hlvl_dev = nullptr;  // its device pointer
   uint32_t* mv_hstate_dev = nullptr;  // device pointer of mv_hlvl + 256 (small-level kernel's state)
   uint32_t* mv_dpair = nullptr;   // [258] level of each expand/apply pair of the predicted loop
-  uint32_t* mv_snapg = nullptr;   // [kept fine bins] the small-level kernel's fills beyond its LDS
   uint32_t* mv_prof = nullptr;    // host-mapped [groups][MV_PROF_WORDS]: the tail kernel's level profile
   uint32_t* mv_prof_dev = nullptr;
   std::vector<std::vector<uint32_t>> mv_pred;  // per group: the last known level sizes (empty: none yet)

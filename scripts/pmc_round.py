@@ -10,6 +10,16 @@ import collections
 import csv
 import json
 import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kernel_hash():
+    """The hash of the kernel sources this profile measured (bench.py checks it)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.load_pkg().kernel_hash()
 
 
 def load(path, counter):
@@ -58,7 +68,7 @@ def main():
     else:
         f = per_round(fr, fam, a.marker, r0, r1)
         w = per_round(wr, fam, a.marker, r0, r1)
-    out = {"kernels": fam, "rounds": [r0, r1], "fetch_size_kib_raw_per_round": f, "write_size_kib_raw_per_round": w,
+    out = {"kernels": fam, "kernel_hash": kernel_hash(), "rounds": [r0, r1], "fetch_size_kib_raw_per_round": f, "write_size_kib_raw_per_round": w,
            "fetch_bytes_corrected": f * 1024 * 2, "write_bytes": w * 1024,
            "traffic_bytes_per_launch": f * 1024 * 2 + w * 1024, "launch": "one round of the family",
            "correction": "FETCH_SIZE x2, WRITE_SIZE as is (profiles/r02/fetch_calibration.json); KiB -> bytes"}

@@ -16,6 +16,16 @@ import collections
 import csv
 import json
 import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kernel_hash():
+    """The hash of the kernel sources this profile measured (bench.py checks it)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.load_pkg().kernel_hash()
 
 
 def per_dispatch(path, kernel, counter):
@@ -42,6 +52,7 @@ def main():
     wk = sum(write) / len(write)
     out = {
         "kernel": a.kernel,
+        "kernel_hash": kernel_hash(),
         "launches_averaged": len(fetch),
         "bench_args": a.bench_args,
         "fetch_size_kib_raw": fk,

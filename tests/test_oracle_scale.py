@@ -156,3 +156,107 @@ def test_rounds_match_oracle_with_engine_active_sets_100k():
     assert int(w_src.max()) >= 65536  # ids beyond u16
     for e in engs.values():
         e.close()
+
+
+# ------------------------------------------- 100k: C4's sweep semantics, gs_round ----
+C4_SLOTS = [  # (origin stake rank, fail fraction, prune-stake threshold, min-ingress)
+    (1, 0.3, 0.15, 2),   # the fail-nodes sweep (when-to-fail 0): failed peers burn their slot
+    (1, 0.0, 0.05, 1),   # the threshold sweep's ends, with other min-ingress values
+    (1, 0.0, 0.40, 3),
+    (2, 0.1, 0.15, 2),   # a second origin with failures
+    (1, 0.5, 0.25, 2),
+]
+
+
+@pytest.mark.parametrize("mode", [gs.GS_BFS_MULTI, gs.GS_BFS_BINNED])
+def test_c4_sweep_semantics_match_oracle_100k(mode):
+    """BASELINE C4's semantics at 100k nodes against the oracle, through the production
+    round (gs_round: the BFS, k_cg_consume, k_cg_prune, the statistics kernels), with the
+    sweep values as slots of ONE engine: fail fractions 0.3 / 0.1 / 0.5 at when-to-fail 0
+    (gossip_main.rs:449-452; Cluster::fail_nodes gossip.rs:756-771; a failed peer burns its
+    fanout slot, gossip.rs:527-541), thresholds 0.05 .. 0.40 and min-ingress 1 / 2 / 3
+    (ReceivedCache::prune, received_cache.rs:100-131), two origins. One oracle sim per slot
+    holds the engine's active sets (p = 0). For 22 rounds, through the first prune wave:
+    failed sets, hops, inbound (src, hop) lists, prunes, counters, prune state, received
+    caches and the per-round summaries' integer fields."""
+    n, seed, rounds = 100_000, 0x5EED0011, 22
+    st = eb.synth.power_law_stakes(n)
+    rank_order = np.lexsort((np.arange(n), -st.astype(np.float64)))
+    S = len(C4_SLOTS)
+    origins = [int(rank_order[r - 1]) for r, _, _, _ in C4_SLOTS]
+    fr = [f for _, f, _, _ in C4_SLOTS]
+    thr = [t for _, _, t, _ in C4_SLOTS]
+    mi = [m for _, _, _, m in C4_SLOTS]
+    eng = gs.Engine(st, S, rotation_probability=0.0, seed=seed, bfs_mode=mode)
+    eng.set_slots(origins, mi, thr)
+    eng.init_active_sets()
+    peers, lens = eng.active_sets()
+    pks = stand_in_pubkeys(n)
+
+    def make_sim(k):
+        s = ob.Sim(ob.PHILOX, seed, pks, st, 6)
+        s.set_entries(peers, lens)
+        assert s.fail_nodes(fr[k]) == int(fr[k] * n)  # when-to-fail 0: before the first BFS
+        return s
+
+    with ThreadPoolExecutor(max_workers=S) as ex:
+        sims = list(ex.map(make_sim, range(S)))
+    del peers, lens
+    eng.fail_nodes(fr)
+    for k, s in enumerate(sims):
+        np.testing.assert_array_equal(eng.failed(k), s.failed(), err_msg=f"failed set slot {k}")
+    pruned_total = [0] * S
+
+    def oracle_round(k, full):  # the reference's round for slot k (the C calls release the GIL)
+        s, o = sims[k], origins[k]
+        s.run_gossip(o)
+        w = {"mn": s.rmr_mn(), "stranded": len(s.stranded()), "dist": s.distances(), "orders": s.orders_all(64 * n)}
+        s.consume_messages(o)  # (send_prunes adds the prunes to RMR's m: read above)
+        s.send_prunes(o, thr[k], mi[k])
+        w["prunes"] = s.prunes()
+        if full:
+            w["caches"] = s.caches(o)
+        s.prune_connections()
+        w["counters"] = s.counters()
+        w["pruned"] = s.pruned_all(o)
+        return w
+
+    with ThreadPoolExecutor(max_workers=S) as ex:
+        for r in range(rounds):
+            full = r % 5 == 0 or 18 <= r <= 20 or r == rounds - 1
+            futs = [ex.submit(oracle_round, k, full) for k in range(S)]
+            eng.round(r, record=True)
+            summ_r = eng.summaries()[r]
+            for k in range(S):
+                w = futs[k].result()
+                np.testing.assert_array_equal(eng.distances(k), w["dist"], err_msg=f"hops slot {k} round {r}")
+                w_off, w_src, w_hop = w["orders"]
+                off, src, hop = eng.inbound(k, cap=len(w_src) + 1)
+                np.testing.assert_array_equal(off, w_off, err_msg=f"in-degrees slot {k} round {r}")
+                np.testing.assert_array_equal(src[:len(w_src)], w_src, err_msg=f"inbound sources slot {k} round {r}")
+                np.testing.assert_array_equal(hop[:len(w_hop)], w_hop, err_msg=f"inbound hops slot {k} round {r}")
+                pruned_total[k] += len(w["prunes"])
+                assert eng.prunes(k) == w["prunes"], f"prunes slot {k} round {r}"
+                if full:
+                    up, ln, keys, sc = eng.caches(k)
+                    oup, oln, okeys, osc = w["caches"]
+                    has = oup != 0xFFFFFFFF
+                    np.testing.assert_array_equal(up[has], oup[has], err_msg=f"upserts slot {k} round {r}")
+                    np.testing.assert_array_equal(up[~has], 0)
+                    np.testing.assert_array_equal(ln, oln, err_msg=f"cache lengths slot {k} round {r}")
+                    np.testing.assert_array_equal(keys, okeys, err_msg=f"cache keys slot {k} round {r}")
+                    np.testing.assert_array_equal(sc, osc, err_msg=f"cache scores slot {k} round {r}")
+                eg, ig, pr = eng.counters(k)
+                oe, oi, op = w["counters"]
+                np.testing.assert_array_equal(eg, np.where(oe == U64MAX, 0, oe), err_msg=f"egress slot {k} round {r}")
+                np.testing.assert_array_equal(ig, np.where(oi == U64MAX, 0, oi), err_msg=f"ingress slot {k} round {r}")
+                np.testing.assert_array_equal(pr, op, err_msg=f"prune-sent slot {k} round {r}")
+                np.testing.assert_array_equal(eng.pruned_all(k), w["pruned"], err_msg=f"prune state slot {k} round {r}")
+                # the round summary's integers (gossip_main.rs:480-563): RMR m / n, stranded, prunes
+                m_, n_ = w["mn"]
+                sm = summ_r[k]
+                assert int(sm["pushes"]) == m_ and int(sm["visited"]) == n_, (k, r, sm, m_, n_)
+                assert int(sm["stranded"]) == w["stranded"], (k, r)
+                assert int(sm["prunes"]) == len(w["prunes"]), (k, r)
+    assert all(p > 0 for p in pruned_total), pruned_total  # every slot went through a prune wave
+    eng.close()
