@@ -14,14 +14,15 @@ waves, where pushes per origin-round settle near 3N).
 value = pushes to non-failed peers over all slots and ranks / wall time of the K
 timed steps (max over ranks).
 
-Multi-GPU (one process per GPU): the ranks split the 3,000 origins of ONE network
-(same seed, so the same active-set trajectory; rank r takes origins [r*S/K,
-(r+1)*S/K)): "strong" scaling, and with --check-shard rank 0 checks the gathered
-per-round summaries of every origin against all origins run on one engine.
---per-rank-networks gives every rank its own 3,000-origin network instead (seed +
-rank, "weak"). --workload c4 deals BASELINE C4's 13 sweep sims (1M nodes) over the
-ranks instead (sweep sharding). torch.distributed carries only the barrier, the
-timing max/sum and the summary gather.
+Multi-GPU (one process per GPU, no data-path collective). Default --scaling weak: the
+ranks shard a sweep of independent C2 trials -- rank r runs all 3,000 origins of the same
+stake network with Philox seed + r (its own active-set trajectory), so the per-GPU work is
+one C2 at every N (origin / parameter slices are independent units).
+--scaling strong: the ranks split the 3,000 origins of ONE trial (same seed; rank r takes
+origins [r*S/K, (r+1)*S/K)), and with --check-shard rank 0 checks the gathered per-round
+summaries of every origin against all origins run on one engine. --workload c4 deals
+BASELINE C4's 13 sweep sims (1M nodes) over the ranks instead. torch.distributed carries
+only the barrier, the timing max/sum and the summary gather.
 
 roofline: the dominant kernel (k_round_wg) with SURVEY.md 8(d) algorithmic bytes
 per launch, divided by that kernel's average duration measured with hipEvents on
@@ -217,7 +218,8 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
     if os.environ.get("GS_PHASE_PROFILE") == "1":  # multi gather: workgroup-ms per phase (thread 0 of each workgroup)
         names = {12: "count", 13: "scan_place", 14: "body_light", 15: "body_all",
                  0: "small_setup", 1: "small_expand_loads", 2: "small_atomics_places", 3: "small_lt_barrier",
-                 4: "small_levels_e-5"}
+                 4: "small_levels_e-5", 5: "lv_setup", 6: "lv_loads", 7: "lv_atomics_stores", 8: "lv_barrier",
+                 9: "lv_levels_e-5"}
         phases = {nm: round(eng.kernel_time("phase." + chr(65 + i))[0], 2) for i, nm in names.items()}
     info = eng.info()
     eng.close()
@@ -412,17 +414,24 @@ def main():
     ap.add_argument("--no-large", action="store_true", help="skip the c4 / c3 legs")
     ap.add_argument("--only-large", action="store_true", help="run only the c4 / c3 legs (A/B of BFS modes)")
     ap.add_argument("--legs", default="c4,c3", help="with --only-large: which legs (e.g. c4 for a PMC pass)")
-    ap.add_argument("--shard-origins", action="store_true",
-                    help="ranks split the origins of ONE network (strong scaling; the default with WORLD_SIZE > 1)")
-    ap.add_argument("--per-rank-networks", action="store_true",
-                    help="with WORLD_SIZE > 1: every rank runs all origins of its own network (seed + rank, weak)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: rank r runs C2 trial r (all origins, Philox seed + r); strong: the ranks split the "
+                         "origins of one trial")
+    ap.add_argument("--shard-origins", action="store_true", help="= --scaling strong")
+    ap.add_argument("--per-rank-networks", action="store_true", help="= --scaling weak")
     ap.add_argument("--check-shard", action="store_true",
                     help="with origin sharding: rank 0 re-runs all origins on one engine and compares")
     ap.add_argument("--workload", default="c2", choices=["c2", "c4"],
                     help="c4: BASELINE C4's 13 sims (1M nodes) dealt round-robin over the ranks (sweep sharding)")
     args = ap.parse_args()
-    if not args.per_rank_networks:
-        args.shard_origins = True  # one network, its origins split over the ranks (all of them at N = 1)
+    if args.shard_origins:
+        args.scaling = "strong"
+    elif args.per_rank_networks:
+        args.scaling = "weak"
+    # strong: one trial's origins split over the ranks; weak: rank r = trial r (all origins,
+    # seed + r). At N = 1 both are the same run.
+    args.shard_origins = args.scaling == "strong"
+    args.per_rank_networks = args.scaling == "weak"
 
     gs = load_pkg()          # loads libgossip_hip.so (and its HIP runtime) before torch, if torch is used at all
     gs.lib()
@@ -582,7 +591,8 @@ def main():
                    "rounds": [args.warmup, args.warmup + args.steps],
                    "pushes_per_origin_round": E_all / (S * world * args.steps) if not args.shard_origins
                    else E_all / (S_all * args.steps),
-                   "parallelism": f"origin-sharded x{world}" + (" (one network)" if args.shard_origins else "")},
+                   "parallelism": (f"origin-sharded x{world} (one trial)" if args.shard_origins else
+                                   f"trial-sharded x{world} (rank r: all origins, Philox seed + r)")},
         "origin_rounds_per_s": (S_all if args.shard_origins else S * world) * args.steps / dt,
         "roofline": roof,
         **({"steady_state": steady} if steady else {}),

@@ -87,6 +87,7 @@ struct MvArgs {
   uint32_t lane_c, wave_c, record;
   unsigned long long* pclk;  // GS_PHASE_PROFILE: gather phase clocks at [12..15] (thread 0 of each workgroup)
   uint32_t gh;  // gather: nodes with more records (all slots) take the wave path
+  uint32_t grows;  // gather: rows in lockstep over the wave (every store one row, coalesced) instead of per-lane appends
   // nodes with per-pair state [vlo, vhi) (= fine bins [flo, flo + fno)); pair = slot * NP + node - vlo.
   // A node-range partition rank runs the whole BFS but keeps the records, counts and
   // egress of its own nodes only.
@@ -638,6 +639,186 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
       __hip_atomic_store(&a.hlvl[k], a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ----------------------------------------------------- persistent levels ----
+// The small levels as ONE launch over the whole chip: G resident workgroups (one per CU),
+// a grid barrier between levels. A level's entries are dealt over every CU, so its
+// device-scope atomics (vis ORs, pool places, next-level reservations) and scattered row
+// loads are spread over 256 address units instead of one CU's (k_mv_small's levels are
+// bound by one CU's rate of scattered accesses: ~20 us for a level of 217 entries at C4).
+// Per level the same steps as k_mv_small (mv_expand_entry, the vis atomic that sets a
+// slot's bit is that slot's first arrival at hop d + 1, gossip.rs:594-600; records to
+// their fine bins' pools stamped with the hop); next-level entries are reserved once per
+// wave on lvl[d + 1] and written to the global queue. Modes as k_mv_small's.
+constexpr uint32_t MV_PT = 512;       // threads per workgroup of the persistent kernel
+// barrier block (e.mv_bar, 256 words): shard counters at 16 s (s < 8), top 128, generation 144, base 160
+constexpr uint32_t MV_PSMALL = 16384;   // default head / tail level bound of the persistent kernel
+
+// Grid barrier of a persistent launch (Guideline 16's counter form, sharded by blockIdx & 7):
+// every wave drains its global stores and atomics, thread 0 releases (agent), arrives on its
+// shard; the last of a shard arrives on the top counter, the last shard publishes the
+// generation e; thread 0 polls it relaxed, then acquires (agent) for the workgroup.
+// Counters are cumulative: epoch e's arrivals end at e x (workgroups of the shard), so no
+// word is reset between barriers or launches (the grid size G of an engine never changes;
+// the last epoch used is kept in word 160 for the next launch). A spin is bounded (~1 s):
+// on expiry ERR_SYNC is raised and the workgroup goes on (wrong results, no hang).
+__device__ inline void mv_grid_sync(uint32_t* bar, uint32_t e, uint32_t G, uint32_t* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the fence's own wait can be dropped: keep it)
+    const uint32_t sh = blockIdx.x & 7u, ns = min(G, 8u), cs = (G - sh + 7u) / 8u;
+    const uint32_t r = __hip_atomic_fetch_add(&bar[16 * sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (r + 1u == e * cs) {
+      const uint32_t t = __hip_atomic_fetch_add(&bar[128], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1u == e * ns) __hip_atomic_store(&bar[144], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (uint32_t it = 0; __hip_atomic_load(&bar[144], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != e; ++it) {
+      if (it > (1u << 22)) {
+        atomicOr(err, ERR_SYNC);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <int ASZP>
+__global__ __launch_bounds__(MV_PT, 4) void k_mv_levels(MvArgs a, uint32_t mode, uint32_t d0, uint32_t pi,
+                                                     uint2* __restrict__ q0, uint2* __restrict__ q1,
+                                                     uint32_t* __restrict__ hstate, const uint2* __restrict__ seeds,
+                                                     uint32_t nseed, uint32_t seq, uint32_t* __restrict__ bar) {
+  __shared__ uint32_t sorg[32], sfk[32], gt[GT_WORDS], s_base, s_qn;
+  const uint32_t tid = threadIdx.x, G = gridDim.x, lane = tid & 63;
+  const uint32_t gtid = blockIdx.x * MV_PT + tid, GT = G * MV_PT;
+  if (tid < a.Sg) {
+    sorg[tid] = a.origin[a.s0 + tid];
+    sfk[tid] = a.fk[a.s0 + tid];
+  }
+  for (uint32_t i = tid; i < GT_WORDS; i += MV_PT) gt[i] = a.gt[i];
+  if (tid == 0) s_base = __hip_atomic_load(&bar[160], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // GS_PHASE_PROFILE: clocks of workgroup 0's thread 0 at pclk[5..8] (setup, the first
+  // chunk's loads, atomics + stores, barriers; [9] levels)
+  const bool clk = a.pclk && blockIdx.x == 0 && tid == 0;
+  unsigned long long tm = clk ? wall_clock64() : 0;
+  auto mark = [&](int ph) {
+    if (clk) {
+      const unsigned long long now = wall_clock64();
+      atomicAdd(&a.pclk[ph], now - tm);
+      tm = now;
+    }
+  };
+  uint32_t d = mode == MV_TAIL ? a.dpair[pi] : d0;
+  if (mode == MV_HEAD) {  // the group's round starts here: lvl, pool fills, the seeds' vis and queue
+    for (uint32_t i = gtid; i < 256; i += GT) a.lvl[i] = i == 0 ? nseed : 0u;
+    for (uint32_t f = gtid; f < a.fno; f += GT) a.pused[f] = 0;
+    if (gtid == 0) a.ctr[0] = 0;
+    if (gtid < nseed) {
+      const uint2 sd = seeds[gtid];  // distinct origins (vis was cleared before this kernel)
+      q0[gtid] = sd;
+      a.vis[sd.x & 0xFFFFFFu] = sd.y;
+    }
+  }
+  __syncthreads();
+  uint32_t ep = s_base;
+  if (mode == MV_HEAD) mv_grid_sync(bar, ++ep, G, a.err);
+  if (tid == 0) s_qn = d < 256 ? __hip_atomic_load(&a.lvl[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  __syncthreads();
+  uint32_t qn = min(s_qn, (uint32_t)a.q_cap);
+  const uint32_t lim = mode == MV_TAIL ? 0xFFFFFFFFu : a.small;
+  mark(5);
+  while (qn > 0 && qn <= lim && d < 254) {
+    if (clk) atomicAdd(&a.pclk[9], 1ull);
+    const uint2* __restrict__ qc = (d & 1) ? q1 : q0;
+    uint2* __restrict__ qx = (d & 1) ? q0 : q1;
+    // 64-entry chunks dealt over the workgroups first (chunk c -> workgroup c mod G, wave
+    // c / G): a level of a few thousand entries runs on as many CUs as it has chunks
+    const uint32_t wbase = (((tid >> 6) * G + blockIdx.x) << 6);
+    for (uint32_t i0 = wbase; i0 < qn; i0 += GT) {  // (uniform per wave: wave scans below)
+      const uint32_t i = i0 + lane;
+      uint32_t row[ASZP], acc[ASZP], u = 0;
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
+      if (i < qn) mv_expand_entry<ASZP>(a, qc[i], sorg, sfk, row, acc, u);
+      if (clk && i0 == wbase) {  // (profiling only: wait for the entry's loads)
+        uint32_t x = 0;
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s) x |= acc[s];
+        if (x == 0xFFFFFFFFu) atomicOr(a.err, 0u);
+        mark(6);
+      }
+      // every global access of the entry before any result is used: the vis atomics, the
+      // peers' buckets, the pool places
+      uint32_t old[ASZP], pp[ASZP], bw[ASZP];
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) old[s] = acc[s] ? atomicOr(&a.vis[row[s]], acc[s]) : 0xFFFFFFFFu;
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) bw[s] = acc[s] ? (uint32_t)a.bucket[row[s]] : 0u;
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        const uint32_t f = (row[s] >> a.BSF) - a.flo;
+        pp[s] = acc[s] && f < a.fno ? atomicAdd(&a.pused[f], 1u) : 0xFFFFFFFFu;  // kept bins only
+      }
+      uint32_t n = 0;
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        const uint32_t nw = acc[s] & ~old[s];
+        if (nw) n += mv_parts(gt, row[s], nw, bw[s], nullptr, 0);
+      }
+      const uint32_t incl = wave_incl_scan(n);
+      const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+      uint32_t wb = 0;
+      if (lane == 63 && tot) wb = atomicAdd(&a.lvl[d + 1], tot);
+      uint32_t pos = (uint32_t)__shfl((int)wb, 63) + incl - n;
+      const bool qok = (size_t)pos + n <= a.q_cap;
+      if (!qok) atomicOr(a.err, ERR_MV_CAP);
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        if (!acc[s]) continue;
+        const uint32_t w = row[s];
+        if (pp[s] != 0xFFFFFFFFu) {
+          const uint32_t f = (w >> a.BSF) - a.flo;
+          if (pp[s] < a.pcap) a.pool[(size_t)f * a.pcap + pp[s]] = mv_pool_rec(a, u, w & ((1u << a.BSF) - 1), d + 1, acc[s]);
+          else atomicOr(a.err, ERR_MV_CAP);
+        }
+        const uint32_t nw = acc[s] & ~old[s];
+        if (nw && qok) pos += mv_parts(gt, w, nw, bw[s], qx, pos);
+      }
+    }
+    mark(7);
+    mv_grid_sync(bar, ++ep, G, a.err);
+    mark(8);
+    ++d;
+    if (tid == 0) s_qn = __hip_atomic_load(&a.lvl[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    qn = min(s_qn, (uint32_t)a.q_cap);
+  }
+  if (blockIdx.x != 0 || tid != 0) return;
+  if (mode == MV_TAIL && qn > 0) atomicOr(a.err, ERR_DEPTH);  // level 254 not empty
+  if (mode == MV_HEAD) a.dpair[0] = d;
+  if (mode == MV_TAIL) {  // the round's level profile for the host's next prediction (seqlock)
+    uint32_t* hp = a.hprof;
+    const uint32_t nl = min(d, 255u);
+    __hip_atomic_store(&hp[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    for (uint32_t k = 0; k < nl; ++k)
+      __hip_atomic_store(&hp[2 + k], __hip_atomic_load(&a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hp[1], nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hp[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (mode != MV_TAIL)  // per-level sizes for the polled loop / diagnostics
+    for (uint32_t k = d0; k < d && k < 256; ++k)
+      __hip_atomic_store(&a.hlvl[k], __hip_atomic_load(&a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (ep != s_base) __hip_atomic_store(&bar[160], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&hstate[1], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&hstate[0], d, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // the host polls this word
+}
+
 // --------------------------------------------------------------- gather ----
 constexpr uint32_t MV_GC = 12;        // records per gather thread kept in registers between the passes
 constexpr uint32_t MV_GLDS_DEF = 78 * 1024;  // gather LDS: two workgroups per CU (GS_MV_GLDS_KB: tuning)
@@ -858,6 +1039,42 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a) {
       const uint32_t v = v0 + i, r0 = L.cn[i] - base, r1 = min(L.cn[i + 1] - base, gcap);
       if (r1 - r0 > a.gh) {
         hvl[atomicAdd(&L.ctl[14], 1u)] = i;
+        continue;
+      }
+      if (a.grows) {
+        // lockstep rows: each trip of the outer loop every live lane stores its next record,
+        // so the trip's store is row `trip` of the wave's 64 consecutive pairs (coalesced)
+        for (uint32_t j = 0; j < Sg; ++j) {
+          const size_t p = (size_t)(a.s0 + j) * a.NP + (v - a.vlo);
+          uint32_t cc = 0, mh = 0xFFu, r = r0;
+          bool live = true;
+          while (__any(live)) {
+            if (!live) continue;
+            uint32_t pos = r1;
+            for (; r < r1; r += 4) {  // the next record of slot j: 4 mask loads per wait
+              uint32_t b = 0;
+#pragma unroll
+              for (int t = 0; t < 4; ++t) b |= ((L.msk[r + t] >> j) & 1u) << t;
+              b &= r1 - r < 4 ? (1u << (r1 - r)) - 1 : 0xFu;
+              if (b) {
+                pos = r + __builtin_ctz(b);
+                break;
+              }
+            }
+            if (pos < r1) {
+              const uint32_t key = L.keys[pos];
+              if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = key;
+              mh = min(mh, key >> 24);
+              ++cc;
+              r = pos + 1;
+            } else {
+              live = false;
+            }
+          }
+          over |= cc > a.capin;
+          a.cnt[p] = cc;
+          a.hops[p] = (uint8_t)(v == L.sorg[j] ? 0u : (cc ? mh : 0xFFu));
+        }
         continue;
       }
       for (uint32_t j = 0; j < Sg; ++j) {
@@ -1147,7 +1364,7 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
   a.vlo = e.vlo; a.vhi = e.vlo + e.NP; a.NP = e.NP; a.MSU = (uint32_t)e.msu;
-  a.small = MV_SMALL;
+  a.small = e.mv_pgrid ? MV_PSMALL : MV_SMALL;  // the persistent kernel's bound, or the one-workgroup kernel's
   if (const char* sm = std::getenv("GS_MV_SMALL")) a.small = (uint32_t)std::strtoul(sm, nullptr, 10);
   if (e.prm.flags & GS_FLAG_NO_SMALL_LEVELS) a.small = 0;  // every level through expand + apply
   a.flo = e.vlo >> e.mv.BSF; a.fno = mv_kept_bins(e);
@@ -1162,6 +1379,8 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.wave_c = narrow ? 8u : 64u;
   a.gh = narrow ? 4u : 256u;  // C4: 291 us with no wave path, 311 at 32
   if (const char* x = std::getenv("GS_MV_GH")) a.gh = (uint32_t)std::strtoul(x, nullptr, 10);
+  a.grows = 0;
+  if (const char* x = std::getenv("GS_MV_GROWS")) a.grows = (uint32_t)std::strtoul(x, nullptr, 10);
   a.pclk = e.phase_clk;
   a.record = 0;
   a.PAIRS = e.PAIRS; a.area_cap = e.mv.area_cap; a.rows_cap = e.mv.rows_cap; a.q_cap = e.mv.q_cap;
@@ -1206,6 +1425,20 @@ hipError_t level_empty(Engine& e, uint32_t d, bool& empty) {
   return r;
 }
 
+// The small-level kernel: the persistent one over the chip (e.mv_pgrid workgroups), or
+// with GS_MV_PERSIST=0 the one-workgroup k_mv_small.
+static void launch_small_levels(Engine& e, const MvArgs& a, uint32_t mode, uint32_t d0, uint32_t pi,
+                                const uint2* seeds, uint32_t nseed, uint32_t seq, size_t lds_s) {
+  if (e.mv_pgrid) {
+    GS_ASZP_DISPATCH_V(e.ASZP, hipLaunchKernelGGL((k_mv_levels<A>), dim3(e.mv_pgrid), dim3(MV_PT), 0, e.st, a, mode,
+                                                  d0, pi, e.mv_q[0], e.mv_q[1], e.mv_hstate_dev, seeds, nseed, seq,
+                                                  e.mv_bar));
+  } else {
+    GS_ASZP_DISPATCH_V(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, mode, d0,
+                                                  pi, e.mv_q[0], e.mv_q[1], e.mv_hstate_dev, seeds, nseed, seq));
+  }
+}
+
 // The level loop of one slot group. Two forms:
 //  - predicted (the group has a level profile from an earlier round): everything is
 //    enqueued at once and the host never waits -- the head kernel (seed + levels of at
@@ -1229,9 +1462,7 @@ static hipError_t mv_group_polled(Engine& e, MvArgs& a, const MvGroup& gr, uint3
   for (;;) {
     // small levels in one workgroup, until the frontier is empty or large
     hs[0] = MV_PENDING;
-    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a,
-                                                head ? MV_HEAD : MV_POLL, d, 0u, e.mv_q[0], e.mv_q[1],
-                                                e.mv_hstate_dev, e.mv_seed + gr.seed0, gr.nseed, 0u));
+    launch_small_levels(e, a, head ? MV_HEAD : MV_POLL, d, 0u, e.mv_seed + gr.seed0, gr.nseed, 0u, lds_s);
     head = false;
     e.bfs_level = d;
     if ((r = mv_wait(hs, e.st, d))) return r;
@@ -1284,6 +1515,18 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       r = hipFuncSetAttribute((const void*)k_mv_small<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s);
     });
     if (r != hipSuccess) return r;
+    // the persistent level kernel: one workgroup per CU, all resident (its grid barriers
+    // need every workgroup running); GS_MV_PERSIST=0 keeps the one-workgroup kernel
+    e.mv_pgrid = 0;
+    const char* px = std::getenv("GS_MV_PERSIST");
+    if (!(px && px[0] == '0')) {
+      int dev = 0, cus = 0, per = 0;
+      if ((r = hipGetDevice(&dev)) || (r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)))
+        return r;
+      GS_ASZP_DISPATCH(e.ASZP, { r = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mv_levels<A>, MV_PT, 0); });
+      if (r != hipSuccess) return r;
+      if (per >= 1 && cus >= 8) e.mv_pgrid = (uint32_t)cus;
+    }
     e.mv_attr_set = true;
   }
   const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8;
@@ -1292,9 +1535,9 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
   uint32_t lag = 2;
   if (const char* x = std::getenv("GS_MV_LAG")) lag = std::max<uint32_t>(1, (uint32_t)std::strtoul(x, nullptr, 10));
   static const bool polled_only = std::getenv("GS_MV_POLLED") && std::getenv("GS_MV_POLLED")[0] == '1';
-  static const uint32_t tail_thr = [] {  // levels the profile had at or below this run in the tail kernel
+  static const uint32_t tail_env = [] {  // levels the profile had at or below this run in the tail kernel
     const char* x = std::getenv("GS_MV_TAIL");
-    return x ? (uint32_t)std::strtoul(x, nullptr, 10) : 2048u;
+    return x ? (uint32_t)std::strtoul(x, nullptr, 10) : 0xFFFFFFFFu;
   }();
   for (uint32_t g = 0; g < (uint32_t)e.mv_groups.size(); ++g) {
     const MvGroup& gr = e.mv_groups[g];
@@ -1337,22 +1580,20 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     } else {
       // the head kernel stops at the first level above a.small; pairs then take the levels
       // the profile had above the tail threshold
+      const uint32_t tail_thr = tail_env != 0xFFFFFFFFu ? tail_env : e.mv_pgrid ? a.small : 2048u;
       uint32_t k0 = 0;
       while (k0 < pv.size() && pv[k0] <= a.small) ++k0;
       uint32_t k1 = (uint32_t)pv.size();  // one past the last level above the tail threshold
       while (k1 > k0 && pv[k1 - 1] <= tail_thr) --k1;
       const uint32_t npairs = std::min<uint32_t>(k1 - k0 + mv_margin(), 250);
-      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, MV_HEAD, 0u,
-                                                  0u, e.mv_q[0], e.mv_q[1], e.mv_hstate_dev, e.mv_seed + gr.seed0,
-                                                  gr.nseed, 0u));
+      launch_small_levels(e, a, MV_HEAD, 0u, 0u, e.mv_seed + gr.seed0, gr.nseed, 0u, lds_s);
       for (uint32_t i = 0; i < npairs; ++i) {
         GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, 0u,
                                                     i, e.mv_q[0], e.mv_q[1]));
         hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, 0u, i, e.mv_q[0], e.mv_q[1]);
       }
       const uint32_t seq = ++e.mv_seq ? e.mv_seq : ++e.mv_seq;  // (never 0)
-      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, MV_TAIL, 0u,
-                                                  npairs, e.mv_q[0], e.mv_q[1], e.mv_hstate_dev, nullptr, 0u, seq));
+      launch_small_levels(e, a, MV_TAIL, 0u, npairs, nullptr, 0u, seq, lds_s);
     }
     e.tend("bfs", t0);
     e.tbegin(consume ? "gather_consume" : "gather", &t0);

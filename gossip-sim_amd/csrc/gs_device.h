@@ -11,7 +11,7 @@ namespace gs {
 
 constexpr int NB = 25;  // NUM_PUSH_ACTIVE_SET_ENTRIES (push_active_set.rs:11)
 constexpr uint32_t P_INIT = 1, P_ROTATE = 2, P_DECIDE = 3, P_FAIL = 4;
-constexpr uint32_t ERR_INBOUND = 1u, ERR_CACHE = 2u, ERR_DEPTH = 4u, ERR_MV_CAP = 8u;
+constexpr uint32_t ERR_INBOUND = 1u, ERR_CACHE = 2u, ERR_DEPTH = 4u, ERR_MV_CAP = 8u, ERR_SYNC = 16u;
 constexpr uint32_t CACHE_CAP = 96;   // >= 50 zero-score + 2 timely keys x 20 rounds (received_cache.rs:78-97)
 constexpr uint32_t CACHE_LIMIT = 50; // ReceivedCacheEntry::CAPACITY
 constexpr uint32_t MIN_NUM_UPSERTS = 20;

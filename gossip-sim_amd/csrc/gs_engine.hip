@@ -138,6 +138,9 @@ static int check_err(Engine* e) {
   if (f & ERR_DEPTH) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
   if (f & ERR_MV_CAP)
     return fail(GS_ERANGE, "multi-source BFS: record / frontier capacity exceeded (recreate with GS_BFS_LEVEL)");
+  if (f & ERR_SYNC)
+    return fail(GS_EHIP, "multi-source BFS: a grid barrier of the persistent level kernel timed out (workgroups not "
+                         "co-resident?); rerun with GS_MV_PERSIST=0");
   if (f & ERR_BOUNDS) return fail(GS_ERANGE, "debug bounds check failed (see GS_OOB lines on stdout)");
   return GS_OK;
 }
@@ -362,6 +365,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     b0 = e->dev_bytes;
     ALLOC(e->mv_pool, (size_t)fno * g.pcap, 0);
     ALLOC(e->mv_pused, fno, 0);
+    ALLOC(e->mv_bar, 256, 0);  // the persistent level kernel's barrier words (MV_BAR_WORDS)
     e->pair_bytes += e->dev_bytes - b0;
     ALLOC(e->mv_fcls, N, 0xFF);
     ALLOC(e->mv_fk, S, 0);

@@ -133,6 +133,8 @@ struct Engine {
   uint2* mv_seed = nullptr;       // [S] seed entries (distinct origins) of every group
   std::vector<MvGroup> mv_groups;
   bool mv_attr_set = false;
+  uint32_t mv_pgrid = 0;          // workgroups of the persistent level kernel (one per CU); 0: one-workgroup kernel
+  uint32_t* mv_bar = nullptr;     // [256] its grid-barrier words (cumulative epochs, zeroed at create)
   uint32_t bfs_level = 0;  // the level loop's current level (reported when a level wait times out)
   bool mv_diag = false;  // GS_MV_DIAG=1
   bool mv_line = false;   // multi: prune masks live in the row table's node lines (msu = 32)
@@ -186,6 +188,19 @@ struct Engine {
   void tend(const char* fam, hipEvent_t a);
 };
 
+// (the same in a function returning void; unsupported sizes are refused at create)
+#define GS_ASZP_DISPATCH_V(ASZP_VAL, CALL)        \
+  switch (ASZP_VAL) {                             \
+    case 4: { constexpr int A = 4; CALL; } break; \
+    case 8: { constexpr int A = 8; CALL; } break; \
+    case 12: { constexpr int A = 12; CALL; } break; \
+    case 16: { constexpr int A = 16; CALL; } break; \
+    case 20: { constexpr int A = 20; CALL; } break; \
+    case 24: { constexpr int A = 24; CALL; } break; \
+    case 28: { constexpr int A = 28; CALL; } break; \
+    case 32: { constexpr int A = 32; CALL; } break; \
+    default: break;                               \
+  }
 #define GS_ASZP_DISPATCH(ASZP_VAL, CALL)          \
   switch (ASZP_VAL) {                             \
     case 4: { constexpr int A = 4; CALL; } break; \
