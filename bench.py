@@ -192,6 +192,9 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
     origin = int(np.argmax(stakes))  # origin rank 1
     fr = [0.1, 0.2, 0.3, 0.4, 0.5] + [0.0] * 8
     thr = [args.threshold] * 5 + [round(0.05 * (j + 1), 2) for j in range(8)]
+    if args.c4_sims:  # one rank's share of the sweep (DESIGN 7's multi-GPU predictions)
+        pick = [int(x) for x in args.c4_sims.split(",")]
+        fr, thr = [fr[i] for i in pick], [thr[i] for i in pick]
     S = len(fr)
     eng = gs.Engine(stakes, S, fanout=args.fanout, active_set_size=args.active_set_size,
                     rotation_probability=0.013333, seed=args.seed, device=0, profile=True, bfs_mode=args.large_mode)
@@ -242,12 +245,13 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
                                      "B_prop (SURVEY 8d), summed over slots", f"bfs_{mode}_c4")}
 
 
-def c5_leg(gs, synth, args, nodes=10_000_000, slots=16, warmup=3, steps=10):
+def c5_leg(gs, synth, args, nodes=10_000_000, slots=None, warmup=3, steps=10):
     """BASELINE C5 as configured, on one GPU: a 10M-node network, origin ranks 1..16 as 16
     slots of ONE engine (the multi-source BFS over one slot group). A node-range partition
     over K ranks divides the per-(slot, node) state; every rank runs this whole BFS
     (DESIGN.md section 7), so the propagation figures are the per-GPU work of C5."""
     import numpy as np
+    slots = slots or args.c5_slots
     stakes = synth.power_law_stakes(nodes)
     order = np.lexsort((np.arange(nodes), -stakes.astype(np.float64)))  # rank order, ties by id
     origins = [int(x) for x in order[:slots]]
@@ -414,6 +418,8 @@ def main():
     ap.add_argument("--no-large", action="store_true", help="skip the c4 / c3 legs")
     ap.add_argument("--only-large", action="store_true", help="run only the c4 / c3 legs (A/B of BFS modes)")
     ap.add_argument("--legs", default="c4,c3", help="with --only-large: which legs (e.g. c4 for a PMC pass)")
+    ap.add_argument("--c4-sims", default="", help="c4 leg: only these of the 13 sweep sims (e.g. 0,8: a rank's share)")
+    ap.add_argument("--c5-slots", type=int, default=16, help="c5 leg: origin ranks 1..K as slots (16 = C5)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: rank r runs C2 trial r (all origins, Philox seed + r); strong: the ranks split the "
                          "origins of one trial")

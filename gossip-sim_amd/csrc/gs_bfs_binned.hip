@@ -161,7 +161,9 @@ __host__ __device__ inline size_t bin_expand_lds_bytes(uint32_t nbins, uint32_t 
 // binned levels. The gather places the binned levels' records after these slots.
 constexpr uint32_t BIN_MIN_FRONTIER = 1u << 17;
 
-template <int ASZP>
+// WG: run by the single-workgroup kernel (k_bin_small): its atomics are workgroup scope
+// (executed in the XCD's L2, atomic_or_wg); the grid-wide expand's are device scope.
+template <int ASZP, bool WG = false>
 __device__ inline void bin_direct(const BinArgs& a, uint32_t d, uint32_t qn, const uint32_t* __restrict__ qcur,
                                   uint32_t* __restrict__ qnxt) {
   const uint32_t rec_hop = (d + 1) << 24;
@@ -185,8 +187,9 @@ __device__ inline void bin_direct(const BinArgs& a, uint32_t d, uint32_t qn, con
     for (int s = 0; s < ASZP; ++s) {  // all atomics back to back, then their results
       const uint32_t q = qb + row[s];
       const bool on = (pm >> s) & 1u;
-      slot[s] = on ? atomicAdd(&a.cnt[q], 1u) : 0u;
-      vold[s] = on ? atomicOr(&a.visbm[q >> 5], 1u << (q & 31)) : ~0u;
+      slot[s] = on ? (WG ? atomic_add_wg(&a.cnt[q], 1u) : atomicAdd(&a.cnt[q], 1u)) : 0u;
+      vold[s] = on ? (WG ? atomic_or_wg(&a.visbm[q >> 5], 1u << (q & 31)) : atomicOr(&a.visbm[q >> 5], 1u << (q & 31)))
+                   : ~0u;
     }
     uint32_t newm = 0;
 #pragma unroll
@@ -204,7 +207,7 @@ __device__ inline void bin_direct(const BinArgs& a, uint32_t d, uint32_t qn, con
     const uint32_t incl = wave_incl_scan(k);
     const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
     uint32_t qbase = 0;
-    if (lane_id() == 63 && tot) qbase = atomicAdd(&a.lvl[d + 1], tot);
+    if (lane_id() == 63 && tot) qbase = WG ? atomic_add_wg(&a.lvl[d + 1], tot) : atomicAdd(&a.lvl[d + 1], tot);
     uint32_t pos = (uint32_t)__shfl((int)qbase, 63) + incl - k;
 #pragma unroll
     for (int s = 0; s < ASZP; ++s)
@@ -240,7 +243,7 @@ __global__ __launch_bounds__(BIN_ST) void k_bin_small(BinArgs a, uint32_t mode, 
   uint32_t qn = s_qn;
   while (qn > 0 && qn <= lim && d < 254) {
     if (threadIdx.x == 0 && mode == BIN_POLL) __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    bin_direct<ASZP>(a, d, qn, (d & 1) ? q1 : q0, (d & 1) ? q0 : q1);
+    bin_direct<ASZP, true>(a, d, qn, (d & 1) ? q1 : q0, (d & 1) ? q0 : q1);
     __syncthreads();
     if (threadIdx.x == 0) s_qn = __hip_atomic_load(&a.lvl[d + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();

@@ -87,7 +87,6 @@ struct MvArgs {
   uint32_t lane_c, wave_c, record;
   unsigned long long* pclk;  // GS_PHASE_PROFILE: gather phase clocks at [12..15] (thread 0 of each workgroup)
   uint32_t gh;  // gather: nodes with more records (all slots) take the wave path
-  uint32_t grows;  // gather: rows in lockstep over the wave (every store one row, coalesced) instead of per-lane appends
   // nodes with per-pair state [vlo, vhi) (= fine bins [flo, flo + fno)); pair = slot * NP + node - vlo.
   // A node-range partition rank runs the whole BFS but keeps the records, counts and
   // egress of its own nodes only.
@@ -255,7 +254,7 @@ __global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, uint3
   const uint32_t G = (qn + MV_XT - 1) / MV_XT;
   if (blockIdx.x >= G) return;  // idle workgroups leave before any setup
   if (G > a.rows_cap) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.err, ERR_MV_CAP);
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.err, ERR_MV_CAP | ERR_MVD_ROWS);
     return;
   }
   const uint32_t tid = threadIdx.x, nb = a.nbc, BSC = a.BSC, UB = a.UB, BPm = (1u << BSC) - 1;
@@ -279,10 +278,14 @@ __global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, uint3
     for (int s = 0; s < ASZP; ++s) rk[s] = acc[s] ? atomicAdd(&hist[row[s] >> BSC], 1u) : 0u;
     __syncthreads();
     const uint32_t total = mv_block_scan(hist, nb, hist + nb);
+    // the slice's run at a fixed place (an entry pushes to at most ASZ distinct peers): no
+    // device-wide counter, which ~2,700 slices of a peak level would queue on (one word
+    // takes ~88 returning atomics per us)
     if (tid == 0) {
-      uint32_t base = atomicAdd(a.ctr, total);
-      if ((size_t)base + total > a.area_cap) {
-        atomicOr(a.err, ERR_MV_CAP);
+      const size_t b64 = (size_t)w * MV_XT * a.ASZ;
+      uint32_t base = (uint32_t)b64;
+      if (b64 + total > a.area_cap) {
+        atomicOr(a.err, ERR_MV_CAP | ERR_MVD_AREA);
         base = 0xFFFFFFFFu;
       }
       sbase = base;
@@ -367,7 +370,11 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
   // fine bin of this coarse bin, reserved once per wave per fine bin
   const uint32_t FS = a.BSC - a.BSF, NF = 1u << FS, f0 = c << FS;
   uint32_t* fcur = ctl + 32;  // [NF <= 16] records appended this level
-  if (tid < NF) fcur[tid] = 0;
+  uint32_t* fbase = ctl + 48;  // [NF] the fine bins' pool fills before this level
+  if (tid < NF) {
+    fcur[tid] = 0;
+    fbase[tid] = f0 + tid - a.flo < a.fno ? a.pused[f0 + tid - a.flo] : 0u;
+  }
   bool loaded = false;  // vis is read only by bins that receive records at this level
   for (uint32_t c0 = 0; c0 < G; c0 += MV_SEG) {
     const uint32_t gc = min(MV_SEG, G - c0);
@@ -391,28 +398,37 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
       loaded = true;
     }
     __syncthreads();
-    for (uint32_t r0 = 0; r0 < ct; r0 += MV_AT) {  // uniform trips: the fine-bin ballots need whole waves
-      const uint32_t r = r0 + tid;
-      const bool live = r < ct;
-      uint32_t lo = 0, hi = gc;  // largest i with pre[i] <= r
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pre[mid] <= r) lo = mid; else hi = mid;
+    // MV_AR records per thread per trip: their searches and area loads are issued
+    // together, so a trip waits for one memory round trip, not MV_AR
+    constexpr uint32_t MV_AR = 4;
+    for (uint32_t r0 = 0; r0 < ct; r0 += MV_AT * MV_AR) {
+      unsigned long long rec[MV_AR];
+#pragma unroll
+      for (uint32_t k = 0; k < MV_AR; ++k) {
+        const uint32_t r = r0 + k * MV_AT + tid;
+        uint32_t lo = 0, hi = gc;  // largest i with pre[i] <= r
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pre[mid] <= r) lo = mid; else hi = mid;
+        }
+        rec[k] = r < ct ? a.area[sb[lo] + (r - pre[lo])] : ~0ull;
       }
-      const unsigned long long rec = live ? a.area[sb[lo] + (r - pre[lo])] : 0ull;
-      uint32_t vl = (uint32_t)(rec >> UB) & BPm;
-      if (live && GS_OOB(vl, nv, a.err, "multi record node")) vl = 0;
-      if (live) atomicOr(&visL[vl], (uint32_t)(rec >> (UB + BSC)));
-      const uint32_t fb = live && f0 + (vl >> a.BSF) - a.flo < a.fno ? vl >> a.BSF : 0xFFFFu;  // kept bins only
-      // the record's place in its fine bin's run: one LDS atomic per lane (measured faster
-      // than one per wave and fine bin by ballots: 19.5-19.7 vs 21.2-24.5 us per launch at C4)
-      const uint32_t pos = fb != 0xFFFFu ? atomicAdd(&fcur[fb], 1u) : 0u;
-      if (fb != 0xFFFFu) {
-        const uint32_t fl = f0 + fb - a.flo;
-        const size_t pp = (size_t)a.pused[fl] + pos;
+#pragma unroll
+      for (uint32_t k = 0; k < MV_AR; ++k) {
+        const bool live = r0 + k * MV_AT + tid < ct;
+        if (!live) continue;
+        uint32_t vl = (uint32_t)(rec[k] >> UB) & BPm;
+        if (GS_OOB(vl, nv, a.err, "multi record node")) vl = 0;
+        const uint32_t m = (uint32_t)(rec[k] >> (UB + BSC));
+        atomicOr(&visL[vl], m);
+        const uint32_t fb = vl >> a.BSF;
+        if (f0 + fb - a.flo >= a.fno) continue;  // kept fine bins only
+        // the record's place in its fine bin's run: one LDS atomic per lane (measured faster
+        // than one per wave and fine bin by ballots: 19.5-19.7 vs 21.2-24.5 us per launch at C4)
+        const size_t pp = (size_t)fbase[fb] + atomicAdd(&fcur[fb], 1u);
         if (pp < a.pcap)
-          a.pool[(size_t)fl * a.pcap + pp] = mv_pool_rec(a, (uint32_t)rec & ((1u << UB) - 1), vl & ((1u << a.BSF) - 1),
-                                                         d + 1, (uint32_t)(rec >> (UB + BSC)));
+          a.pool[(size_t)(f0 + fb - a.flo) * a.pcap + pp] =
+              mv_pool_rec(a, (uint32_t)rec[k] & ((1u << UB) - 1), vl & ((1u << a.BSF) - 1), d + 1, m);
       }
     }
     __syncthreads();
@@ -420,9 +436,9 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
   __syncthreads();
   if (tid < NF && f0 + tid - a.flo < a.fno) {  // each kept fine bin's pool fill
     const uint32_t fl = f0 + tid - a.flo;
-    const uint32_t used = a.pused[fl], n = fcur[tid];
+    const uint32_t used = fbase[tid], n = fcur[tid];
     const bool over = (size_t)used + n > a.pcap;
-    if (over) atomicOr(a.err, ERR_MV_CAP);
+    if (over) atomicOr(a.err, ERR_MV_CAP | ERR_MVD_POOL);
     if (n) a.pused[fl] = over ? (uint32_t)a.pcap : used + n;
   }
   if (!loaded) return;  // no records: no first arrivals in this bin
@@ -444,7 +460,7 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
   if (tid == 0) {
     const uint32_t base = atomicAdd(&a.lvl[d + 1], tnew);
     ctl[1] = base;
-    if ((size_t)base + tnew > a.q_cap) { atomicOr(a.err, ERR_MV_CAP); ctl[1] = 0xFFFFFFFFu; }
+    if ((size_t)base + tnew > a.q_cap) { atomicOr(a.err, ERR_MV_CAP | ERR_MVD_Q); ctl[1] = 0xFFFFFFFFu; }
   }
   __syncthreads();
   if (ctl[1] == 0xFFFFFFFFu) return;
@@ -567,14 +583,14 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
       // without LDS fills, the pool-place atomics
       uint32_t old[ASZP], pp[ASZP], bw[ASZP];
 #pragma unroll
-      for (int s = 0; s < ASZP; ++s) old[s] = acc[s] ? atomicOr(&a.vis[row[s]], acc[s]) : 0xFFFFFFFFu;
+      for (int s = 0; s < ASZP; ++s) old[s] = acc[s] ? atomic_or_wg(&a.vis[row[s]], acc[s]) : 0xFFFFFFFFu;
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) bw[s] = acc[s] ? (uint32_t)a.bucket[row[s]] : 0u;
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) {
         const uint32_t f = (row[s] >> a.BSF) - a.flo;
         const bool kept = acc[s] && f < a.fno;  // kept bins only
-        pp[s] = !kept ? 0xFFFFFFFFu : LP ? atomicAdd(&lp[f], 1u) : atomicAdd(&a.pused[f], 1u);
+        pp[s] = !kept ? 0xFFFFFFFFu : LP ? atomicAdd(&lp[f], 1u) : atomic_add_wg(&a.pused[f], 1u);
       }
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) {
@@ -586,7 +602,7 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
           if (pp[s] < a.pcap)
             a.pool[(size_t)f * a.pcap + pp[s]] = mv_pool_rec(a, u, w & ((1u << a.BSF) - 1), d + 1, acc[s]);
           else
-            atomicOr(a.err, ERR_MV_CAP);
+            atomicOr(a.err, ERR_MV_CAP | ERR_MVD_POOL);
         }
         if (nw) {  // this thread's first arrivals at w (another thread may add more bits to w)
           const uint32_t n = mv_parts(gt, w, nw, bw[s], nullptr, 0);
@@ -597,7 +613,7 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
               else qgn[base + k] = x;
             });
           } else {
-            atomicOr(a.err, ERR_MV_CAP);
+            atomicOr(a.err, ERR_MV_CAP | ERR_MVD_Q);
           }
         }
       }
@@ -653,10 +669,14 @@ constexpr uint32_t MV_PT = 512;       // threads per workgroup of the persistent
 // barrier block (e.mv_bar, 256 words): shard counters at 16 s (s < 8), top 128, generation 144, base 160
 constexpr uint32_t MV_PSMALL = 16384;   // default head / tail level bound of the persistent kernel
 
-// Grid barrier of a persistent launch (Guideline 16's counter form, sharded by blockIdx & 7):
-// every wave drains its global stores and atomics, thread 0 releases (agent), arrives on its
-// shard; the last of a shard arrives on the top counter, the last shard publishes the
-// generation e; thread 0 polls it relaxed, then acquires (agent) for the workgroup.
+// Grid barrier of a persistent launch (Guideline 16's counter form, sharded by blockIdx & 7).
+// Everything one workgroup hands to another inside the launch is written through to memory
+// and read around L1: the next level's queue entries by agent-scope (sc1) stores and loads,
+// the level sizes, visited masks and pool fills by device-scope atomics. So the barrier
+// needs no L2 write-back (release fence) and no L1 invalidate (acquire fence): every wave
+// drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier, thread 0 arrives on
+// its shard; the last of a shard arrives on the top counter, the last shard publishes the
+// generation e (an atomic store); thread 0 polls it relaxed.
 // Counters are cumulative: epoch e's arrivals end at e x (workgroups of the shard), so no
 // word is reset between barriers or launches (the grid size G of an engine never changes;
 // the last epoch used is kept in word 160 for the next launch). A spin is bounded (~1 s):
@@ -665,8 +685,6 @@ __device__ inline void mv_grid_sync(uint32_t* bar, uint32_t e, uint32_t G, uint3
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the fence's own wait can be dropped: keep it)
     const uint32_t sh = blockIdx.x & 7u, ns = min(G, 8u), cs = (G - sh + 7u) / 8u;
     const uint32_t r = __hip_atomic_fetch_add(&bar[16 * sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (r + 1u == e * cs) {
@@ -680,10 +698,22 @@ __device__ inline void mv_grid_sync(uint32_t* bar, uint32_t e, uint32_t G, uint3
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+}
+
+// Agent-scope (sc1: through L2 to memory, around L1) 8-byte queue entry store / load.
+__device__ inline void mv_q_store(uint2* p, uint2 x) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)x.x | ((unsigned long long)x.y << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline uint2 mv_q_load(const uint2* p) {
+  const unsigned long long v =
+      __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+__device__ inline void mv_st_agent(uint32_t* p, uint32_t x) {
+  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int ASZP>
@@ -713,13 +743,13 @@ __global__ __launch_bounds__(MV_PT, 4) void k_mv_levels(MvArgs a, uint32_t mode,
   };
   uint32_t d = mode == MV_TAIL ? a.dpair[pi] : d0;
   if (mode == MV_HEAD) {  // the group's round starts here: lvl, pool fills, the seeds' vis and queue
-    for (uint32_t i = gtid; i < 256; i += GT) a.lvl[i] = i == 0 ? nseed : 0u;
-    for (uint32_t f = gtid; f < a.fno; f += GT) a.pused[f] = 0;
+    for (uint32_t i = gtid; i < 256; i += GT) mv_st_agent(&a.lvl[i], i == 0 ? nseed : 0u);
+    for (uint32_t f = gtid; f < a.fno; f += GT) mv_st_agent(&a.pused[f], 0u);
     if (gtid == 0) a.ctr[0] = 0;
     if (gtid < nseed) {
       const uint2 sd = seeds[gtid];  // distinct origins (vis was cleared before this kernel)
-      q0[gtid] = sd;
-      a.vis[sd.x & 0xFFFFFFu] = sd.y;
+      mv_q_store(&q0[gtid], sd);
+      mv_st_agent(&a.vis[sd.x & 0xFFFFFFu], sd.y);
     }
   }
   __syncthreads();
@@ -742,7 +772,7 @@ __global__ __launch_bounds__(MV_PT, 4) void k_mv_levels(MvArgs a, uint32_t mode,
       uint32_t row[ASZP], acc[ASZP], u = 0;
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
-      if (i < qn) mv_expand_entry<ASZP>(a, qc[i], sorg, sfk, row, acc, u);
+      if (i < qn) mv_expand_entry<ASZP>(a, mv_q_load(&qc[i]), sorg, sfk, row, acc, u);
       if (clk && i0 == wbase) {  // (profiling only: wait for the entry's loads)
         uint32_t x = 0;
 #pragma unroll
@@ -774,7 +804,7 @@ __global__ __launch_bounds__(MV_PT, 4) void k_mv_levels(MvArgs a, uint32_t mode,
       if (lane == 63 && tot) wb = atomicAdd(&a.lvl[d + 1], tot);
       uint32_t pos = (uint32_t)__shfl((int)wb, 63) + incl - n;
       const bool qok = (size_t)pos + n <= a.q_cap;
-      if (!qok) atomicOr(a.err, ERR_MV_CAP);
+      if (!qok) atomicOr(a.err, ERR_MV_CAP | ERR_MVD_Q);
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) {
         if (!acc[s]) continue;
@@ -782,10 +812,10 @@ __global__ __launch_bounds__(MV_PT, 4) void k_mv_levels(MvArgs a, uint32_t mode,
         if (pp[s] != 0xFFFFFFFFu) {
           const uint32_t f = (w >> a.BSF) - a.flo;
           if (pp[s] < a.pcap) a.pool[(size_t)f * a.pcap + pp[s]] = mv_pool_rec(a, u, w & ((1u << a.BSF) - 1), d + 1, acc[s]);
-          else atomicOr(a.err, ERR_MV_CAP);
+          else atomicOr(a.err, ERR_MV_CAP | ERR_MVD_POOL);
         }
         const uint32_t nw = acc[s] & ~old[s];
-        if (nw && qok) pos += mv_parts(gt, w, nw, bw[s], qx, pos);
+        if (nw && qok) pos += mv_parts_to(gt, w, nw, bw[s], [&](uint32_t k, uint2 x) { mv_q_store(&qx[pos + k], x); });
       }
     }
     mark(7);
@@ -905,7 +935,7 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nv, uint
         }
         h = l2;
       }
-      if (h == lo) { atomicOr(a.err, ERR_MV_CAP); h = nv; }  // one node beyond the LDS CSR
+      if (h == lo) { atomicOr(a.err, ERR_MV_CAP | ERR_MVD_CSR); h = nv; }  // one node beyond the LDS CSR
       ctl[15] = h;
       ctl[14] = 0;  // body's heavy-node count (k_mv_gather)
     }
@@ -1039,42 +1069,6 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a) {
       const uint32_t v = v0 + i, r0 = L.cn[i] - base, r1 = min(L.cn[i + 1] - base, gcap);
       if (r1 - r0 > a.gh) {
         hvl[atomicAdd(&L.ctl[14], 1u)] = i;
-        continue;
-      }
-      if (a.grows) {
-        // lockstep rows: each trip of the outer loop every live lane stores its next record,
-        // so the trip's store is row `trip` of the wave's 64 consecutive pairs (coalesced)
-        for (uint32_t j = 0; j < Sg; ++j) {
-          const size_t p = (size_t)(a.s0 + j) * a.NP + (v - a.vlo);
-          uint32_t cc = 0, mh = 0xFFu, r = r0;
-          bool live = true;
-          while (__any(live)) {
-            if (!live) continue;
-            uint32_t pos = r1;
-            for (; r < r1; r += 4) {  // the next record of slot j: 4 mask loads per wait
-              uint32_t b = 0;
-#pragma unroll
-              for (int t = 0; t < 4; ++t) b |= ((L.msk[r + t] >> j) & 1u) << t;
-              b &= r1 - r < 4 ? (1u << (r1 - r)) - 1 : 0xFu;
-              if (b) {
-                pos = r + __builtin_ctz(b);
-                break;
-              }
-            }
-            if (pos < r1) {
-              const uint32_t key = L.keys[pos];
-              if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = key;
-              mh = min(mh, key >> 24);
-              ++cc;
-              r = pos + 1;
-            } else {
-              live = false;
-            }
-          }
-          over |= cc > a.capin;
-          a.cnt[p] = cc;
-          a.hops[p] = (uint8_t)(v == L.sorg[j] ? 0u : (cc ? mh : 0xFFu));
-        }
         continue;
       }
       for (uint32_t j = 0; j < Sg; ++j) {
@@ -1278,8 +1272,8 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   g.TW = g.nbc + 2;
   const size_t sg = std::min<size_t>(S, g.GW);
   g.q_cap = (size_t)N * std::min<size_t>(sg, 26) + 64;
-  g.area_cap = std::min<size_t>(g.q_cap * ASZ, 0xFFFFFFF0u);
   g.rows_cap = (g.q_cap + MV_XT - 1) / MV_XT + 1;
+  g.area_cap = std::min<size_t>(g.rows_cap * MV_XT * ASZ, 0xFFFFFFF0u);  // expand slice w's run at w * MV_XT * ASZ
   const size_t rpn = (size_t)ASZ * std::min<size_t>(sg, 4) + 16;  // pool records per node (average over a bin)
   g.pcap = ((size_t)1 << g.BSF) * rpn;
   // (4 records' worth of slack: the filters read up to 3 records past a node's list)
@@ -1379,8 +1373,6 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.wave_c = narrow ? 8u : 64u;
   a.gh = narrow ? 4u : 256u;  // C4: 291 us with no wave path, 311 at 32
   if (const char* x = std::getenv("GS_MV_GH")) a.gh = (uint32_t)std::strtoul(x, nullptr, 10);
-  a.grows = 0;
-  if (const char* x = std::getenv("GS_MV_GROWS")) a.grows = (uint32_t)std::strtoul(x, nullptr, 10);
   a.pclk = e.phase_clk;
   a.record = 0;
   a.PAIRS = e.PAIRS; a.area_cap = e.mv.area_cap; a.rows_cap = e.mv.rows_cap; a.q_cap = e.mv.q_cap;
@@ -1515,11 +1507,15 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       r = hipFuncSetAttribute((const void*)k_mv_small<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s);
     });
     if (r != hipSuccess) return r;
-    // the persistent level kernel: one workgroup per CU, all resident (its grid barriers
-    // need every workgroup running); GS_MV_PERSIST=0 keeps the one-workgroup kernel
+    // GS_MV_PERSIST=1: the persistent level kernel (one workgroup per CU, all resident: its
+    // grid barriers need every workgroup running) instead of the one-workgroup kernel. Off
+    // by default: at C4 it saves ~2 % of the BFS (715.6 vs 732 us with levels up to 16,384
+    // entries), while a node reached by several workgroups at one level becomes several
+    // frontier entries (the apply kernel merges them per node), so it expands more entries
+    // and fills the record pools less predictably.
     e.mv_pgrid = 0;
     const char* px = std::getenv("GS_MV_PERSIST");
-    if (!(px && px[0] == '0')) {
+    if (px && px[0] == '1') {
       int dev = 0, cus = 0, per = 0;
       if ((r = hipGetDevice(&dev)) || (r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)))
         return r;

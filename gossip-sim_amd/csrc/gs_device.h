@@ -12,6 +12,9 @@ namespace gs {
 constexpr int NB = 25;  // NUM_PUSH_ACTIVE_SET_ENTRIES (push_active_set.rs:11)
 constexpr uint32_t P_INIT = 1, P_ROTATE = 2, P_DECIDE = 3, P_FAIL = 4;
 constexpr uint32_t ERR_INBOUND = 1u, ERR_CACHE = 2u, ERR_DEPTH = 4u, ERR_MV_CAP = 8u, ERR_SYNC = 16u;
+// which multi-source BFS capacity ERR_MV_CAP hit (reported with it)
+constexpr uint32_t ERR_MVD_ROWS = 0x1000u, ERR_MVD_AREA = 0x2000u, ERR_MVD_POOL = 0x4000u, ERR_MVD_Q = 0x8000u,
+                   ERR_MVD_CSR = 0x10000u;
 constexpr uint32_t CACHE_CAP = 96;   // >= 50 zero-score + 2 timely keys x 20 rounds (received_cache.rs:78-97)
 constexpr uint32_t CACHE_LIMIT = 50; // ReceivedCacheEntry::CAPACITY
 constexpr uint32_t MIN_NUM_UPSERTS = 20;
@@ -222,6 +225,18 @@ __device__ inline uint32_t taken_slots(const uint32_t (&row)[ASZP], uint32_t hea
 }
 
 __device__ inline uint32_t lane_id() { return __lane_id(); }
+
+// Atomics for words that only ONE workgroup touches during the kernel (the single-
+// workgroup level kernels): workgroup scope, so they execute in the XCD's L2 instead of
+// at the memory side (a device-scope returning atomic is a fabric round trip: the small
+// levels' atomics at C4 took ~10 us per level). Data from earlier kernels is visible and
+// the results reach later kernels through the kernel-boundary write-back as usual.
+__device__ inline uint32_t atomic_or_wg(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline uint32_t atomic_add_wg(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // Inclusive prefix sum over the 64 lanes of a wave (all lanes must be active).
 __device__ inline uint32_t wave_incl_scan(uint32_t x) {

@@ -131,16 +131,23 @@ static int check_err(Engine* e) {
   HIPC(hipMemcpyAsync(e->h_err, e->err, 4, hipMemcpyDeviceToHost, e->st));
   HIPC(hipStreamSynchronize(e->st));
   const uint32_t f = e->h_err[0];
+  if (f & ERR_SYNC)  // (first: a barrier that timed out leaves every later result suspect)
+    return fail(GS_EHIP, "multi-source BFS: a grid barrier of the persistent level kernel timed out (workgroups not "
+                         "co-resident?); rerun without GS_MV_PERSIST=1");
   if (f & ERR_INBOUND)
     return fail(GS_ERANGE, "inbound capacity exceeded: a node received more than " + std::to_string(e->capin) +
                                " pushes in one round; recreate the engine with a larger inbound_capacity");
   if (f & ERR_CACHE) return fail(GS_ERANGE, "received-cache capacity (96 keys) exceeded");
   if (f & ERR_DEPTH) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
-  if (f & ERR_MV_CAP)
-    return fail(GS_ERANGE, "multi-source BFS: record / frontier capacity exceeded (recreate with GS_BFS_LEVEL)");
-  if (f & ERR_SYNC)
-    return fail(GS_EHIP, "multi-source BFS: a grid barrier of the persistent level kernel timed out (workgroups not "
-                         "co-resident?); rerun with GS_MV_PERSIST=0");
+  if (f & ERR_MV_CAP) {
+    std::string what;
+    if (f & ERR_MVD_ROWS) what += " level rows";
+    if (f & ERR_MVD_AREA) what += " level records";
+    if (f & ERR_MVD_POOL) what += " record pool";
+    if (f & ERR_MVD_Q) what += " frontier queue";
+    if (f & ERR_MVD_CSR) what += " gather CSR (one node's records)";
+    return fail(GS_ERANGE, "multi-source BFS: capacity exceeded:" + what + " (recreate with GS_BFS_LEVEL)");
+  }
   if (f & ERR_BOUNDS) return fail(GS_ERANGE, "debug bounds check failed (see GS_OOB lines on stdout)");
   return GS_OK;
 }
