@@ -8,7 +8,7 @@ import csv
 import os
 import sys
 
-FAM = ['k_round_wg', 'k_mv_expand', 'k_mv_apply', 'k_mv_small', 'k_mv_gather', 'k_mv_consume', 'k_cg_consume', 'k_cg_prune', 'k_bin_expand', 'k_bin_apply', 'k_bin_gather', 'k_stats_pass', 'k_rotate_entries']
+FAM = ['k_round_wg', 'k_mv_expand', 'k_mv_apply', 'k_mv_small', 'k_mv_levels', 'k_mv_gather', 'k_mv_consume', 'k_cg_consume', 'k_cg_prune', 'k_bin_expand', 'k_bin_apply', 'k_bin_gather', 'k_stats_pass', 'k_rotate_entries']
 
 
 def main():

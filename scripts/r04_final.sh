@@ -57,22 +57,22 @@ if has pmc_legs; then
 fi
 
 if has sq; then
+  SQC=SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,TA_BUSY_avr
   d=$OUT/sq
   mkdir -p $d
   echo "== sq k_round_wg"
-  timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU \
-    SQ_INSTS_LDS TA_BUSY_avr --kernel-trace --output-format csv -d $d/c2 -o run -- \
+  timeout -s KILL 300 rocprofv3 --pmc $SQC --kernel-trace --output-format csv -d $d/c2 -o run -- \
     python3 bench.py --warmup 5 --steps 20 --no-cpu-baseline --no-profile --no-large --no-steady > $d/c2.log 2>&1 \
     || { tail -5 $d/c2.log; exit 1; }
   for leg in c4 c5; do
     echo "== sq $leg"
-    timeout -s KILL 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU \
-      SQ_INSTS_LDS TA_BUSY_avr --kernel-trace --output-format csv -d $d/$leg -o run -- \
+    timeout -s KILL 600 rocprofv3 --pmc $SQC --kernel-trace --output-format csv -d $d/$leg -o run -- \
       python3 bench.py --only-large --legs $leg > $d/$leg.log 2>&1 || { tail -5 $d/$leg.log; exit 1; }
   done
-  python3 scripts/pmc_table.py $d/c2/run_counter_collection.csv k_round_wg > $P/sq_k_round_wg_c2.txt 2>&1 || true
-  for leg in c4 c5; do
-    python3 scripts/pmc_table.py $d/$leg/run_counter_collection.csv k_mv_ > $P/sq_bfs_multi_$leg.txt 2>&1 || true
+  KH=$(python3 -c "import bench; print(bench.load_pkg().kernel_hash())")
+  for leg in c2 c4 c5; do
+    { echo "kernel_hash: $KH (SQ/TA counters, one rocprofv3 --pmc pass; bench legs as in r04_final.sh)";
+      python3 scripts/pmc_table.py $d $leg; } > $P/sq_counters_$leg.txt 2>&1 || true
   done
 fi
 
@@ -84,6 +84,15 @@ if has trace; then
     --bench-args "--warmup 5 --steps 20" --out $P/trace_k_round_wg_c2_r5-24.json || exit 1
   cp $OUT/prof/run_kernel_stats.csv $P/rocprof_kernel_stats_driver_window.csv
   grep '"metric"' $OUT/prof.log | tail -1 > $P/bench_driver_window_traced.json
+  echo "== trace legs"
+  timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $OUT/proflegs -o run -- \
+    python3 bench.py --only-large --legs c4,c5 > $OUT/proflegs.log 2>&1 || { tail -20 $OUT/proflegs.log; exit 1; }
+  MVT=k_mv_expand,k_mv_apply,k_mv_small,k_mv_levels,k_mv_gather
+  python3 scripts/trace_window.py --csv $OUT/proflegs/run_kernel_trace.csv --family $MVT --marker k_mv_gather \
+    --rounds 5,24 --bench-args "--only-large --legs c4" --out $P/trace_bfs_multi_c4.json || exit 1
+  # (c5's rounds follow c4's 25 in the same trace: c4 rounds 0-24 end at marker 24)
+  python3 scripts/trace_window.py --csv $OUT/proflegs/run_kernel_trace.csv --family $MVT --marker k_mv_gather \
+    --rounds 28,37 --bench-args "--only-large --legs c5" --out $P/trace_bfs_multi_c5.json || exit 1
 fi
 
 if has bench; then

@@ -30,12 +30,17 @@ def kernel_hash():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--csv", required=True)
-    ap.add_argument("--kernel", required=True, help="substring of the kernel name")
-    ap.add_argument("--first", type=int, required=True, help="index of the first launch kept")
-    ap.add_argument("--count", type=int, required=True)
+    ap.add_argument("--kernel", default="", help="substring of the kernel name")
+    ap.add_argument("--first", type=int, default=0, help="index of the first launch kept")
+    ap.add_argument("--count", type=int, default=0)
+    ap.add_argument("--family", default="", help="family mode: comma-separated kernel names summed per round")
+    ap.add_argument("--marker", default="", help="family mode: the kernel whose dispatches end the rounds")
+    ap.add_argument("--rounds", default="", help="family mode: first,last round (0-based, of the marker's count)")
     ap.add_argument("--bench-args", default="")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
+    if a.family:
+        return family_mode(a)
     rows = []
     with open(a.csv) as f:
         for r in csv.DictReader(f):
@@ -55,6 +60,32 @@ def main():
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "durations_us"}))
+
+
+def family_mode(a):
+    """Per-round device time of a kernel family: the durations of every dispatch of the
+    family between the marker dispatches that end rounds r0-1 and r1 (one engine; the
+    round that a marker dispatch ends is counted from 0), summed per round and averaged --
+    the time a bench leg's bfs_roofline divides by (its hipEvents span the same kernels)."""
+    fam = a.family.split(",")
+    rows = []
+    with open(a.csv) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    ends = [i for i, (_, _, k) in enumerate(rows) if a.marker in k]
+    r0, r1 = (int(x) for x in a.rounds.split(","))
+    per = []
+    for r in range(r0, r1 + 1):
+        lo, hi = (ends[r - 1] + 1 if r else 0), ends[r] + 1
+        per.append(sum(e - s for s, e, k in rows[lo:hi] if any(x in k for x in fam)) / 1e3)
+    out = {"kernels": fam, "marker": a.marker, "kernel_hash": kernel_hash(), "bench_args": a.bench_args,
+           "rounds": [r0, r1], "avg_us": sum(per) / len(per), "min_us": min(per), "max_us": max(per),
+           "per_round_us": [round(x, 1) for x in per], "launch": "one round of the family",
+           "source": "rocprofv3 --kernel-trace (Start/End_Timestamp, ns)"}
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k != "per_round_us"}))
 
 
 if __name__ == "__main__":
