@@ -16,6 +16,9 @@ P=profiles/r04
 mkdir -p $OUT $P
 STEPS=${STEPS:-"pmc_c2 pmc_legs sq trace bench"}
 has() { case " $STEPS " in *" $1 "*) return 0;; *) return 1;; esac; }
+# (the box's profiles/r04 is read by the later steps' bench runs; only gpurun_out/ comes back:
+# every exit copies it there)
+trap 'mkdir -p $OUT/profiles_r04 && cp -r $P/. $OUT/profiles_r04/' EXIT
 
 if has pmc_c2; then
   for win in "5 20" "60 100"; do
