@@ -20,8 +20,9 @@ stake network with Philox seed + r (its own active-set trajectory), so the per-G
 one C2 at every N (origin / parameter slices are independent units).
 --scaling strong: the ranks split the 3,000 origins of ONE trial (same seed; rank r takes
 origins [r*S/K, (r+1)*S/K)), and with --check-shard rank 0 checks the gathered per-round
-summaries of every origin against all origins run on one engine. --workload c4 deals
-BASELINE C4's 13 sweep sims (1M nodes) over the ranks instead. torch.distributed carries
+summaries of every origin against all origins run on one engine. --workload c4 / c5 run
+BASELINE C4's 13 sweep sims (1M nodes) / C5's 16 origins (10M nodes) instead, dealt over
+the ranks (strong) or all on every rank as its own trial (weak). torch.distributed carries
 only the barrier, the timing max/sum and the summary gather.
 
 roofline: the dominant kernel (k_round_wg) with SURVEY.md 8(d) algorithmic bytes
@@ -339,26 +340,50 @@ def c3_leg(gs, synth, args, nodes=100_000, warmup=5, steps=20):
             "bfs_roofline": roofline(bp, b_ms, 2 * steps, f"BFS ({mode})", "B_prop (SURVEY 8d)", f"bfs_{mode}_c3")}
 
 
-def c4_sweep_sharded(gs, synth, args, rank, world, dev, barrier, reduce, nodes=1_000_000):
-    """--workload c4: BASELINE C4's sweep sims (fail-nodes 0.1..0.5 at when-to-fail 0, then
-    prune-stake-threshold 0.05..0.40) dealt round-robin over the ranks (sweep.shard); each
-    rank runs its sims as slots of one engine over the SAME 1M-node network and seed. The
-    total work is fixed (strong scaling); value = all ranks' pushes / the slowest rank's time."""
+def sweep_workload(gs, synth, args, rank, world, dev, barrier, reduce):
+    """--workload c4 | c5 over one process per GPU (independent sims, no
+    data-path collective).
+    c4: BASELINE C4's 13 sweep sims (fail-nodes 0.1..0.5 at when-to-fail 0, then
+        prune-stake-threshold 0.05..0.40) over the 1M-node network;
+    c5: BASELINE C5's 16 origins (stake ranks 1..16) over the 10M-node network.
+    --scaling strong deals the sims round-robin over the ranks (sweep.shard: the total work
+    is fixed); --scaling weak gives every rank all of them as its own trial (Philox seed +
+    rank: the per-GPU work is fixed). Each rank runs its sims as slots of one engine;
+    value = all ranks' pushes / the slowest rank's time."""
     import numpy as np
-    shard = list(range(rank, 13, world))
-    stakes = synth.power_law_stakes(nodes)
-    origin = int(np.argmax(stakes))
-    fr_all = [0.1, 0.2, 0.3, 0.4, 0.5] + [0.0] * 8
-    thr_all = [args.threshold] * 5 + [round(0.05 * (j + 1), 2) for j in range(8)]
+    kind = args.workload
+    if kind == "c4":
+        nodes = 1_000_000
+        stakes = synth.power_law_stakes(nodes)
+        origin = int(np.argmax(stakes))
+        n_all = 13
+        org_all = [origin] * n_all
+        fr_all = [0.1, 0.2, 0.3, 0.4, 0.5] + [0.0] * 8
+        thr_all = [args.threshold] * 5 + [round(0.05 * (j + 1), 2) for j in range(8)]
+        what = ("C4: 1M-node power-law network, origin rank 1, fail-nodes 0.1..0.5 + prune-stake-threshold "
+                "0.05..0.40 (13 sims)")
+    else:
+        nodes = 10_000_000
+        stakes = synth.power_law_stakes(nodes)
+        order = np.lexsort((np.arange(nodes), -stakes.astype(np.float64)))
+        n_all = 16
+        org_all = [int(x) for x in order[:n_all]]
+        fr_all = [0.0] * n_all
+        thr_all = [args.threshold] * n_all
+        what = "C5: 10M-node power-law network, origin ranks 1..16 (16 sims)"
+    weak = args.scaling == "weak"
+    shard = list(range(n_all)) if weak else list(range(rank, n_all, world))
+    seed = args.seed + rank if weak else args.seed
     E = 0.0
     eng = None
     if shard:
         eng = gs.Engine(stakes, len(shard), fanout=args.fanout, active_set_size=args.active_set_size,
-                        rotation_probability=0.013333, seed=args.seed, device=dev, profile=True,
+                        rotation_probability=0.013333, seed=seed, device=dev, profile=True,
                         bfs_mode=args.large_mode)
-        eng.set_slots([origin] * len(shard), args.min_ingress, [thr_all[i] for i in shard])
+        eng.set_slots([org_all[i] for i in shard], args.min_ingress, [thr_all[i] for i in shard])
         eng.init_active_sets()
-        eng.fail_nodes([fr_all[i] for i in shard])  # when-to-fail 0 (gossip_main.rs:449-452)
+        if any(fr_all[i] for i in shard):
+            eng.fail_nodes([fr_all[i] for i in shard])  # when-to-fail 0 (gossip_main.rs:449-452)
         for r in range(args.warmup):
             eng.round(r, record=False)
         eng.sync()
@@ -372,6 +397,7 @@ def c4_sweep_sharded(gs, synth, args, rank, world, dev, barrier, reduce, nodes=1
     barrier()
     dt = reduce(time.perf_counter() - t0, lambda d: d.ReduceOp.MAX)
     roof = None
+    mode = None
     if eng:
         summ = eng.summaries()
         E = float(summ["pushes"].astype("float64").sum())
@@ -382,16 +408,18 @@ def c4_sweep_sharded(gs, synth, args, rank, world, dev, barrier, reduce, nodes=1
         mode = eng.info()["bfs_mode"]
         eng.close()
     E_all = reduce(E, lambda d: d.ReduceOp.SUM)
+    sims_total = n_all * (world if weak else 1)
     return {"metric": METRIC, "value": E_all / dt, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (deterministic Philox power-law stakes, SURVEY.md 8(d))",
-            "config": {"workload": f"C4: {nodes}-node power-law network, origin rank 1, fail-nodes 0.1..0.5 + "
-                                   "prune-stake-threshold 0.05..0.40 (13 sims) dealt round-robin over the ranks",
-                       "nodes": nodes, "sims_total": 13, "sims_rank0": len(shard), "rounds":
-                       [args.warmup, args.warmup + args.steps], "parallelism": f"sweep-sharded x{world} (one network)",
-                       "bfs_mode": mode if shard else None},
-            "origin_rounds_per_s": 13 * args.steps / dt, "roofline_rank0": roof, "cpu_baseline": None}
+            "config": {"workload": what + (" per rank, rank r = Philox seed + r" if weak else
+                                           " dealt round-robin over the ranks"),
+                       "nodes": nodes, "sims_total": sims_total, "sims_rank0": len(shard),
+                       "rounds": [args.warmup, args.warmup + args.steps],
+                       "parallelism": (f"trial-sharded x{world}" if weak else f"sweep-sharded x{world} (one network)"),
+                       "bfs_mode": mode},
+            "origin_rounds_per_s": sims_total * args.steps / dt, "roofline_rank0": roof, "cpu_baseline": None}
 
 
 # ------------------------------------------------------------------------ main ----
@@ -427,8 +455,9 @@ def main():
     ap.add_argument("--per-rank-networks", action="store_true", help="= --scaling weak")
     ap.add_argument("--check-shard", action="store_true",
                     help="with origin sharding: rank 0 re-runs all origins on one engine and compares")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c4"],
-                    help="c4: BASELINE C4's 13 sims (1M nodes) dealt round-robin over the ranks (sweep sharding)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"],
+                    help="c4: BASELINE C4's 13 sims (1M nodes), c5: C5's 16 origins (10M nodes) over the ranks "
+                         "(--scaling strong: dealt round-robin; weak: every rank all of them, seed + rank)")
     args = ap.parse_args()
     if args.shard_origins:
         args.scaling = "strong"
@@ -472,8 +501,8 @@ def main():
         dist[1].all_reduce(t, op=op(dist[1]))
         return float(t.item())
 
-    if args.workload == "c4":
-        out = c4_sweep_sharded(gs, synth, args, rank, world, dev, barrier, reduce)
+    if args.workload in ("c4", "c5"):
+        out = sweep_workload(gs, synth, args, rank, world, dev, barrier, reduce)
         if rank == 0:
             print(json.dumps(out), flush=True)
         if dist:
