@@ -46,7 +46,9 @@ namespace gs {
 
 namespace {
 
-constexpr uint32_t MV_XT = 256;       // expand threads = frontier entries per expand workgroup
+constexpr uint32_t MV_XT = 256;       // expand threads = frontier entries per expand slice (one T row)
+constexpr uint32_t MV_XT_L = 1024;    // ... for wide T rows (>= MV_XT_WIDE coarse bins: 10M-node graphs)
+constexpr uint32_t MV_XT_WIDE = 512;
 constexpr uint32_t MV_AT = 1024;      // apply threads
 constexpr uint32_t MV_GT = 512;       // gather threads
 constexpr uint32_t MV_SEG = 1024;     // T rows per apply chunk
@@ -92,6 +94,7 @@ struct MvArgs {
   // egress of its own nodes only.
   uint32_t vlo, vhi, flo, fno, NP;
   uint32_t MSU;  // node stride of the masks (SP, or 32 in node lines)
+  uint32_t XT;   // frontier entries per expand slice (MV_XT or MV_XT_L; mv_geometry)
   uint32_t small;  // levels of at most this many entries run in the one-workgroup kernel
   size_t PAIRS, area_cap, rows_cap, q_cap, pcap;
 };
@@ -241,9 +244,14 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const uint32_
 
 // Level d (pi == MV_NOPAIR), or pair pi's level dpair[pi] (the predicted loop; 0 entries
 // there when the BFS already ended: a no-op).
-template <int ASZP>
-__global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, uint32_t pi, const uint2* __restrict__ q0,
-                                                     const uint2* __restrict__ q1) {
+// XT entries per slice (= threads): a slice writes one T row of nbc + 2 words and every
+// apply workgroup reads one word of every row, so with thousands of coarse bins (C5: 1,220)
+// the rows cost more than the records; 1,024-entry slices make 4x fewer rows (C5 BFS
+// 9.36 -> 6.95 ms per round) while at C4's 245 bins 256-entry slices stay faster (730 vs
+// 768 us).
+template <int ASZP, uint32_t XT>
+__global__ __launch_bounds__(XT) void k_mv_expand(MvArgs a, uint32_t d, uint32_t pi, const uint2* __restrict__ q0,
+                                                  const uint2* __restrict__ q1) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t sorg[32], sfk[32], sbase;
   if (pi != MV_NOPAIR) d = a.dpair[pi];
@@ -251,7 +259,7 @@ __global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, uint3
   const uint2* __restrict__ qcur = (d & 1) ? q1 : q0;
   if (pi == MV_NOPAIR && blockIdx.x == 0 && threadIdx.x == 0)  // the host's termination poll (host-mapped)
     __hip_atomic_store(&a.hlvl[d], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const uint32_t G = (qn + MV_XT - 1) / MV_XT;
+  const uint32_t G = (qn + XT - 1) / XT;
   if (blockIdx.x >= G) return;  // idle workgroups leave before any setup
   if (G > a.rows_cap) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.err, ERR_MV_CAP | ERR_MVD_ROWS);
@@ -263,14 +271,14 @@ __global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, uint3
     sfk[tid] = a.fk[a.s0 + tid];
   }
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);  // [nb] + scan words
-  unsigned long long* stage = reinterpret_cast<unsigned long long*>(smem + mv_hist_bytes(nb));  // [MV_XT * ASZP]
+  unsigned long long* stage = reinterpret_cast<unsigned long long*>(smem + mv_hist_bytes(nb));  // [XT * ASZP]
   for (uint32_t w = blockIdx.x; w < G; w += gridDim.x) {
-    for (uint32_t i = tid; i < nb; i += MV_XT) hist[i] = 0;
+    for (uint32_t i = tid; i < nb; i += XT) hist[i] = 0;
     __syncthreads();
     uint32_t row[ASZP], acc[ASZP], u = 0;
 #pragma unroll
     for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
-    const uint32_t i = w * MV_XT + tid;
+    const uint32_t i = w * XT + tid;
     if (i < qn) mv_expand_entry<ASZP>(a, qcur[i], sorg, sfk, row, acc, u);
     // every LDS atomic after every load: each record's rank within its coarse bin
     uint32_t rk[ASZP];
@@ -282,7 +290,7 @@ __global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, uint3
     // device-wide counter, which ~2,700 slices of a peak level would queue on (one word
     // takes ~88 returning atomics per us)
     if (tid == 0) {
-      const size_t b64 = (size_t)w * MV_XT * a.ASZ;
+      const size_t b64 = (size_t)w * XT * a.ASZ;
       uint32_t base = (uint32_t)b64;
       if (b64 + total > a.area_cap) {
         atomicOr(a.err, ERR_MV_CAP | ERR_MVD_AREA);
@@ -294,7 +302,7 @@ __global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, uint3
     const uint32_t base = sbase;
     const bool ok = base != 0xFFFFFFFFu;
     uint32_t* Tr = a.T + (size_t)w * a.TW;
-    for (uint32_t b = tid; b < nb; b += MV_XT) Tr[1 + b] = ok ? hist[b] : 0u;
+    for (uint32_t b = tid; b < nb; b += XT) Tr[1 + b] = ok ? hist[b] : 0u;
     if (tid == 0) {
       Tr[0] = ok ? base : 0u;
       Tr[1 + nb] = ok ? total : 0u;
@@ -308,7 +316,7 @@ __global__ __launch_bounds__(MV_XT) void k_mv_expand(MvArgs a, uint32_t d, uint3
       }
     __syncthreads();
     if (ok)
-      for (uint32_t r = tid; r < total; r += MV_XT) a.area[base + r] = stage[r];
+      for (uint32_t r = tid; r < total; r += XT) a.area[base + r] = stage[r];
     __syncthreads();
   }
 }
@@ -358,7 +366,7 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
   const uint32_t c = mv_xcd_bin(blockIdx.x, a.nbc);
   if (c >= a.nbc) return;
   const uint32_t tid = threadIdx.x, BSC = a.BSC, UB = a.UB, BP = 1u << BSC, BPm = BP - 1;
-  const uint32_t G = (qn + MV_XT - 1) / MV_XT;
+  const uint32_t G = (qn + a.XT - 1) / a.XT;
   const uint32_t v0 = c << BSC, nv = min(BP, a.N - v0);
   uint32_t* pre = reinterpret_cast<uint32_t*>(smem);  // [MV_SEG + 1]
   uint32_t* sb = pre + MV_SEG + 1;                    // [MV_SEG]
@@ -1272,8 +1280,9 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   g.TW = g.nbc + 2;
   const size_t sg = std::min<size_t>(S, g.GW);
   g.q_cap = (size_t)N * std::min<size_t>(sg, 26) + 64;
-  g.rows_cap = (g.q_cap + MV_XT - 1) / MV_XT + 1;
-  g.area_cap = std::min<size_t>(g.rows_cap * MV_XT * ASZ, 0xFFFFFFF0u);  // expand slice w's run at w * MV_XT * ASZ
+  g.XT = g.nbc >= MV_XT_WIDE && mv_hist_bytes(g.nbc) + (size_t)MV_XT_L * ASZP * 8 <= 160 * 1024 ? MV_XT_L : MV_XT;
+  g.rows_cap = (g.q_cap + g.XT - 1) / g.XT + 1;
+  g.area_cap = std::min<size_t>(g.rows_cap * g.XT * ASZ, 0xFFFFFFF0u);  // expand slice w's run at w * XT * ASZ
   const size_t rpn = (size_t)ASZ * std::min<size_t>(sg, 4) + 16;  // pool records per node (average over a bin)
   g.pcap = ((size_t)1 << g.BSF) * rpn;
   // (4 records' worth of slack: the filters read up to 3 records past a node's list)
@@ -1282,7 +1291,7 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
 }
 
 bool mv_supported(const MvGeom& g, uint32_t ASZP) {
-  return mv_hist_bytes(g.nbc) + (size_t)MV_XT * ASZP * 8 <= 160 * 1024 && mv_apply_lds_bytes(g.BSC) <= 160 * 1024 &&
+  return mv_hist_bytes(g.nbc) + (size_t)g.XT * ASZP * 8 <= 160 * 1024 && mv_apply_lds_bytes(g.BSC) <= 160 * 1024 &&
          g.GW >= 4;
 }
 
@@ -1358,6 +1367,7 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
   a.vlo = e.vlo; a.vhi = e.vlo + e.NP; a.NP = e.NP; a.MSU = (uint32_t)e.msu;
+  a.XT = e.mv.XT;
   a.small = e.mv_pgrid ? MV_PSMALL : MV_SMALL;  // the persistent kernel's bound, or the one-workgroup kernel's
   if (const char* sm = std::getenv("GS_MV_SMALL")) a.small = (uint32_t)std::strtoul(sm, nullptr, 10);
   if (e.prm.flags & GS_FLAG_NO_SMALL_LEVELS) a.small = 0;  // every level through expand + apply
@@ -1417,6 +1427,17 @@ hipError_t level_empty(Engine& e, uint32_t d, bool& empty) {
   return r;
 }
 
+// One expand launch (slices of e.mv.XT entries).
+static void launch_expand(Engine& e, const MvArgs& a, uint32_t d, uint32_t pi, size_t lds_x, uint32_t xgrid) {
+  if (e.mv.XT == MV_XT_L) {
+    GS_ASZP_DISPATCH_V(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A, MV_XT_L>), dim3(xgrid), dim3(MV_XT_L), lds_x, e.st, a,
+                                                  d, pi, e.mv_q[0], e.mv_q[1]));
+  } else {
+    GS_ASZP_DISPATCH_V(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A, MV_XT>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, d,
+                                                  pi, e.mv_q[0], e.mv_q[1]));
+  }
+}
+
 // The small-level kernel: the persistent one over the chip (e.mv_pgrid workgroups), or
 // with GS_MV_PERSIST=0 the one-workgroup k_mv_small.
 static void launch_small_levels(Engine& e, const MvArgs& a, uint32_t mode, uint32_t d0, uint32_t pi,
@@ -1442,7 +1463,7 @@ static void launch_small_levels(Engine& e, const MvArgs& a, uint32_t mode, uint3
 //  - polled (no profile yet): the host enqueues level d after seeing level d - lag's size.
 static hipError_t mv_group_polled(Engine& e, MvArgs& a, const MvGroup& gr, uint32_t lag, uint32_t& nlev) {
   hipError_t r;
-  const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)MV_XT * e.ASZP * 8;
+  const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)e.mv.XT * e.ASZP * 8;
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
   const uint32_t fno = mv_kept_bins(e);
   const size_t lds_s = fno <= MV_SMALL_LP ? (size_t)fno * 4 : 0;
@@ -1471,8 +1492,7 @@ static hipError_t mv_group_polled(Engine& e, MvArgs& a, const MvGroup& gr, uint3
         return hipSuccess;
       }
       hl[d] = MV_PENDING;
-      GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, d,
-                                                  MV_NOPAIR, e.mv_q[0], e.mv_q[1]));
+      launch_expand(e, a, d, MV_NOPAIR, lds_x, xgrid);
       hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, d, MV_NOPAIR, e.mv_q[0], e.mv_q[1]);
       if (d >= dl + lag) {
         uint32_t x = 0;
@@ -1487,14 +1507,18 @@ static hipError_t mv_group_polled(Engine& e, MvArgs& a, const MvGroup& gr, uint3
 
 hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
   hipError_t r = hipSuccess;
-  const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)MV_XT * e.ASZP * 8;
+  const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)e.mv.XT * e.ASZP * 8;
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
   const size_t lds_g = mv_glds();
   const uint32_t fno = mv_kept_bins(e);
   const size_t lds_s = fno <= MV_SMALL_LP ? (size_t)fno * 4 : 0;
   if (!e.mv_attr_set) {
     GS_ASZP_DISPATCH(e.ASZP, {
-      r = hipFuncSetAttribute((const void*)k_mv_expand<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_x);
+      r = e.mv.XT == MV_XT_L
+              ? hipFuncSetAttribute((const void*)k_mv_expand<A, MV_XT_L>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds_x)
+              : hipFuncSetAttribute((const void*)k_mv_expand<A, MV_XT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds_x);
     });
     if (r != hipSuccess) return r;
     if ((r = hipFuncSetAttribute((const void*)k_mv_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_a)))
@@ -1584,8 +1608,7 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       const uint32_t npairs = std::min<uint32_t>(k1 - k0 + mv_margin(), 250);
       launch_small_levels(e, a, MV_HEAD, 0u, 0u, e.mv_seed + gr.seed0, gr.nseed, 0u, lds_s);
       for (uint32_t i = 0; i < npairs; ++i) {
-        GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_expand<A>), dim3(xgrid), dim3(MV_XT), lds_x, e.st, a, 0u,
-                                                    i, e.mv_q[0], e.mv_q[1]));
+        launch_expand(e, a, 0u, i, lds_x, xgrid);
         hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, 0u, i, e.mv_q[0], e.mv_q[1]);
       }
       const uint32_t seq = ++e.mv_seq ? e.mv_seq : ++e.mv_seq;  // (never 0)

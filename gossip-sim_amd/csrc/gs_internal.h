@@ -36,6 +36,7 @@ struct BinGeom {
 constexpr uint32_t GT_WORDS = 96;  // per-group table words
 struct MvGeom {
   uint32_t UB = 0, BSC = 0, BSF = 0, nbc = 0, nbf = 0, GW = 0, TW = 0, gcap = 0, gcap_c = 0;
+  uint32_t XT = 256;  // frontier entries per expand slice (256, or 1,024 for wide T rows)
   size_t q_cap = 0, area_cap = 0, rows_cap = 0, pcap = 0;
 };
 struct MvGroup { uint32_t s0, sg, seed0, nseed; };
