@@ -218,13 +218,7 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
     for k in ("gather", "gather_consume"):
         if not fam[k]:
             del fam[k]
-    phases = None
-    if os.environ.get("GS_PHASE_PROFILE") == "1":  # multi gather: workgroup-ms per phase (thread 0 of each workgroup)
-        names = {12: "count", 13: "scan_place", 14: "body_light", 15: "body_all",
-                 0: "small_setup", 1: "small_expand_loads", 2: "small_atomics_places", 3: "small_lt_barrier",
-                 4: "small_levels_e-5", 5: "lv_setup", 6: "lv_loads", 7: "lv_atomics_stores", 8: "lv_barrier",
-                 9: "lv_levels_e-5"}
-        phases = {nm: round(eng.kernel_time("phase." + chr(65 + i))[0], 2) for i, nm in names.items()}
+    phases = gather_phases(eng)
     info = eng.info()
     eng.close()
     mode = {2: "level", 3: "binned", 4: "multi"}.get(info["bfs_mode"], str(info["bfs_mode"]))
@@ -244,6 +238,18 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
                                                          ("fused gather/consume)" if "gather_consume" in fam
                                                           else "gather)") if mode == "multi" else "per level)"),
                                      "B_prop (SURVEY 8d), summed over slots", f"bfs_{mode}_c4")}
+
+
+def gather_phases(eng):
+    """GS_PHASE_PROFILE=1 (multi BFS): workgroup-ms per phase (thread 0 of each workgroup),
+    and the pool records the gathers read ("pool_records": the count x 1e-5)."""
+    if os.environ.get("GS_PHASE_PROFILE") != "1":
+        return None
+    names = {12: "count", 13: "scan_place", 14: "body_light", 15: "body_all",
+             0: "small_setup", 1: "small_expand_loads", 2: "small_atomics_places", 3: "small_lt_barrier",
+             4: "small_levels_e-5", 5: "lv_setup", 6: "lv_loads", 7: "lv_atomics_stores", 8: "lv_barrier",
+             9: "lv_levels_e-5", 10: "pool_records"}
+    return {nm: round(eng.kernel_time("phase." + chr(65 + i))[0], 2) for i, nm in names.items()}
 
 
 def c5_leg(gs, synth, args, nodes=10_000_000, slots=None, warmup=3, steps=10):
@@ -276,10 +282,12 @@ def c5_leg(gs, synth, args, nodes=10_000_000, slots=None, warmup=3, steps=10):
     E = float(summ["pushes"].astype("float64").sum())
     V = float(summ["visited"].astype("float64").sum())
     fam = {k: eng.kernel_time(k)[0] for k in ("bfs", "gather", "consume", "rotate", "stats")}
+    phases = gather_phases(eng)
     info = eng.info()
     eng.close()
     mode = {2: "level", 3: "binned", 4: "multi"}.get(info["bfs_mode"], str(info["bfs_mode"]))
-    return {"workload": f"C5 on one GPU: {nodes}-node power-law network, origin ranks 1-{len(origins)} as "
+    return {**({"gather_phases_wg_ms": phases} if phases else {}),
+            "workload": f"C5 on one GPU: {nodes}-node power-law network, origin ranks 1-{len(origins)} as "
                         f"slots of one engine (unpartitioned; every partition rank runs this BFS)",
             "bfs_mode": mode, "rounds": [warmup, warmup + steps], "ms_per_step": dt / steps * 1e3,
             "edges_per_s": E / dt, "origin_rounds_per_s": len(origins) * steps / dt,

@@ -902,6 +902,7 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nv, uint
   for (uint32_t i = tid; i <= BP; i += MV_GT) cn[i] = 0;
   if (tid < a.Sg) L.sorg[tid] = a.origin[a.s0 + tid];
   const uint32_t Etot = min(a.pused[f], (uint32_t)a.pcap);
+  if (a.pclk && tid == 0) atomicAdd(&a.pclk[10], (unsigned long long)Etot);  // (profiling: pool records)
   auto key_of = [&](unsigned long long rec) {
     return (((uint32_t)(rec >> (UB + BSF)) & 0xFFu) << 24) | ((uint32_t)rec & um);
   };
@@ -1055,9 +1056,13 @@ __device__ inline uint32_t mv_pair_hop(const MvCsr& L, uint32_t r0, uint32_t r1,
 }
 
 // Per (slot, node) of the fine bin: in-degree, the inbound rows and the hop (the step
-// API's gs_run_gossip, and gs_round unless GS_MV_FUSED=1). A lane appends its pair's
-// records as it finds them (rows of different lanes differ: measured faster than
-// filtering to a bitmap and storing row t of every lane together, 568 vs 697 us at C4).
+// API's gs_run_gossip, and gs_round unless GS_MV_FUSED=1). A lane holds its node's slot
+// masks in registers, 32 records at a time, and per slot builds a 32-record bitmap from
+// them (two ALU ops per record), then appends the slot's records in list order, one per
+// set bit (round 4; before, every slot re-read and re-tested every record from LDS:
+// ~21 instructions per (slot, record) for ~4.7 set bits per record at C5). Lanes hold
+// consecutive nodes, so a slot's row t of every single-chunk node is stored by the same
+// instruction.
 // A node with more than MV_GH records (all slots) is deferred to a whole wave: stake
 // weights make in-degrees power-law, and one such node in a wave of lanes held the
 // other 63 lanes for its whole list (every slot). (256; 4 under GS_FLAG_NARROW_WAVE_PATH)
@@ -1079,21 +1084,32 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a) {
         hvl[atomicAdd(&L.ctl[14], 1u)] = i;
         continue;
       }
+      const uint32_t vo = v - a.vlo;
+      uint32_t A[32];  // slot masks of 32 records (>= 31 records of slack follow the CSR)
+#pragma unroll
+      for (int t = 0; t < 32; ++t) A[t] = L.msk[r0 + t];
       for (uint32_t j = 0; j < Sg; ++j) {
-        const size_t p = (size_t)(a.s0 + j) * a.NP + (v - a.vlo);
+        uint32_t* __restrict__ row = a.inb + (size_t)(a.s0 + j) * a.NP + vo;
         uint32_t cc = 0, mh = 0xFFu;
-        for (uint32_t r = r0; r < r1; r += 4) {  // 8 LDS loads, then one wait (>= 2 records of slack follow the CSR)
-          uint32_t m[4], k[4];
+        for (uint32_t rb = r0; rb < r1; rb += 32) {
+          if (r1 - r0 > 32 && (rb != r0 || j)) {  // (nodes of more than one chunk)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) { m[t] = L.msk[r + t]; k[t] = L.keys[r + t]; }
+            for (int t = 0; t < 32; ++t) A[t] = L.msk[rb + t];
+          }
+          uint32_t b = 0;
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (r + t >= r1 || !((m[t] >> j) & 1u)) continue;
-            if (cc < a.capin) a.inb[(size_t)cc * a.PAIRS + p] = k[t];
-            mh = min(mh, k[t] >> 24);
+          for (int t = 0; t < 32; ++t) b |= ((A[t] >> j) & 1u) << t;
+          if (r1 - rb < 32) b &= (1u << (r1 - rb)) - 1u;
+          while (b) {
+            const uint32_t pos = (uint32_t)__builtin_ctz(b);
+            b &= b - 1u;
+            const uint32_t key = L.keys[rb + pos];
+            if (cc < a.capin) row[(size_t)cc * a.PAIRS] = key;
+            mh = min(mh, key >> 24);
             ++cc;
           }
         }
+        const size_t p = (size_t)(a.s0 + j) * a.NP + vo;
         over |= cc > a.capin;
         a.cnt[p] = cc;
         a.hops[p] = (uint8_t)(v == L.sorg[j] ? 0u : (cc ? mh : 0xFFu));
@@ -1285,8 +1301,9 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   g.area_cap = std::min<size_t>(g.rows_cap * g.XT * ASZ, 0xFFFFFFF0u);  // expand slice w's run at w * XT * ASZ
   const size_t rpn = (size_t)ASZ * std::min<size_t>(sg, 4) + 16;  // pool records per node (average over a bin)
   g.pcap = ((size_t)1 << g.BSF) * rpn;
-  // (4 records' worth of slack: the filters read up to 3 records past a node's list)
-  g.gcap = (uint32_t)((mv_glds() - mv_gather_fixed_bytes(g.BSF)) / 8) - 4;
+  // (slack: k_mv_gather reads masks up to 31 records past a node's list, the fused
+  // consume's filters up to 3)
+  g.gcap = (uint32_t)((mv_glds() - mv_gather_fixed_bytes(g.BSF)) / 8) - 32;
   g.gcap_c = (uint32_t)((mv_glds() - MV_CSCR - mv_gather_fixed_bytes(g.BSF)) / 8) - 4;
 }
 
@@ -1382,7 +1399,7 @@ static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.lane_c = narrow ? 4u : 16u;
   a.wave_c = narrow ? 8u : 64u;
   a.gh = narrow ? 4u : 256u;  // C4: 291 us with no wave path, 311 at 32
-  if (const char* x = std::getenv("GS_MV_GH")) a.gh = (uint32_t)std::strtoul(x, nullptr, 10);
+  if (const char* x = std::getenv("GS_MV_GH")) a.gh = std::min<uint32_t>(4096, (uint32_t)std::strtoul(x, nullptr, 10));
   a.pclk = e.phase_clk;
   a.record = 0;
   a.PAIRS = e.PAIRS; a.area_cap = e.mv.area_cap; a.rows_cap = e.mv.rows_cap; a.q_cap = e.mv.q_cap;
