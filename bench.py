@@ -245,7 +245,7 @@ def gather_phases(eng):
     and the pool records the gathers read ("pool_records": the count x 1e-5)."""
     if os.environ.get("GS_PHASE_PROFILE") != "1":
         return None
-    names = {12: "count", 13: "scan_place", 14: "body_light", 15: "body_all",
+    names = {12: "count_scan", 13: "range_place", 11: "body_all", 14: "body_light", 15: "body_heavy",
              0: "small_setup", 1: "small_expand_loads", 2: "small_atomics_places", 3: "small_lt_barrier",
              4: "small_levels_e-5", 5: "lv_setup", 6: "lv_loads", 7: "lv_atomics_stores", 8: "lv_barrier",
              9: "lv_levels_e-5", 10: "pool_records"}

@@ -87,7 +87,7 @@ struct MvArgs {
   uint32_t* ingress_acc;
   uint32_t N, SP, ASZ, fanout, capin, s0, Sg, UB, BSC, BSF, nbc, nbf, TW, ORW, any_fail, gcap, gcap_c;
   uint32_t lane_c, wave_c, record;
-  unsigned long long* pclk;  // GS_PHASE_PROFILE: gather phase clocks at [12..15] (thread 0 of each workgroup)
+  unsigned long long* pclk;  // GS_PHASE_PROFILE: gather phase clocks at [11..15] (thread 0 of each workgroup)
   uint32_t gh;  // gather: nodes with more records (all slots) take the wave path
   // nodes with per-pair state [vlo, vhi) (= fine bins [flo, flo + fno)); pair = slot * NP + node - vlo.
   // A node-range partition rank runs the whole BFS but keeps the records, counts and
@@ -925,10 +925,10 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nv, uint
     if (vc[j] != 0xFFFFFFFFu) atomicAdd(&cn[vc[j]], 1u);
   for (uint32_t t = tid + MV_GC * MV_GT; t < Etot; t += MV_GT) atomicAdd(&cn[(uint32_t)(pool[t] >> UB) & BPm], 1u);
   __syncthreads();
-  mark(12);
   const uint32_t E2 = mv_block_scan(cn, BP, ctl);
   if (tid == 0) cn[BP] = E2;
   __syncthreads();
+  mark(12);
   // 2. node ranges whose records fit the LDS CSR (one range unless the bin is heavy); the
   // register-held records are placed in the first range only (they are dead afterwards:
   // later ranges re-read the pool), so they do not stay live across body
@@ -979,12 +979,14 @@ __device__ inline void mv_bin_csr(const MvArgs& a, uint32_t f, uint32_t nv, uint
   mark(13);
   body(0u, hi, 0u);
   __syncthreads();
-  mark(15);
+  mark(11);
   for (uint32_t lo = hi; lo < nv; lo = hi) {
     hi = range(lo);
     place_pool(lo, hi, 0);
+    mark(13);
     body(lo, hi, cn[lo]);
     __syncthreads();
+    mark(11);
   }
 }
 
@@ -1068,7 +1070,10 @@ __device__ inline uint32_t mv_pair_hop(const MvCsr& L, uint32_t r0, uint32_t r1,
 // other 63 lanes for its whole list (every slot). (256; 4 under GS_FLAG_NARROW_WAVE_PATH)
 __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t f = mv_xcd_bin(blockIdx.x, a.fno);  // local kept-bin index
+  // (local kept-bin index, in dispatch order: stakes fall with node id, so the low bins
+  // hold the hubs' long lists; contiguous ranges per XCD left XCD 0 the heavy bins, C5's
+  // gather 5.70 vs 4.41 ms per round)
+  const uint32_t f = blockIdx.x;
   if (f >= a.fno) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, BP = 1u << a.BSF, Sg = a.Sg, v0 = (a.flo + f) << a.BSF;
   if (v0 >= a.vhi) return;
@@ -1100,13 +1105,22 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a) {
 #pragma unroll
           for (int t = 0; t < 32; ++t) b |= ((A[t] >> j) & 1u) << t;
           if (r1 - rb < 32) b &= (1u << (r1 - rb)) - 1u;
-          while (b) {
-            const uint32_t pos = (uint32_t)__builtin_ctz(b);
-            b &= b - 1u;
-            const uint32_t key = L.keys[rb + pos];
-            if (cc < a.capin) row[(size_t)cc * a.PAIRS] = key;
-            mh = min(mh, key >> 24);
-            ++cc;
+          while (b) {  // four set bits per trip: four LDS loads, then their stores
+            uint32_t k[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              ok[u] = b != 0;
+              k[u] = L.keys[rb + (uint32_t)__builtin_ctz(b | 0x80000000u)];  // (b = 0: record 31, in the slack)
+              b &= b - 1u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (!ok[u]) break;
+              if (cc < a.capin) row[(size_t)cc * a.PAIRS] = k[u];
+              mh = min(mh, k[u] >> 24);
+              ++cc;
+            }
           }
         }
         const size_t p = (size_t)(a.s0 + j) * a.NP + vo;
@@ -1116,7 +1130,8 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a) {
       }
     }
     __syncthreads();
-    if (a.pclk && tid == 0) atomicAdd(&a.pclk[14], wall_clock64() - tb);  // the light part ([15]: whole body)
+    const unsigned long long tl = a.pclk && tid == 0 ? wall_clock64() : 0;
+    if (a.pclk && tid == 0) atomicAdd(&a.pclk[14], tl - tb);  // (phase clocks: the light nodes, [15] the heavy)
     // heavy nodes, one per wave: 64 records per step, each slot's ranks by ballot
     const uint32_t nh = L.ctl[14];
     for (uint32_t h = tid >> 6; h < nh; h += MV_GT / 64) {
@@ -1145,6 +1160,10 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a) {
         }
       }
     }
+    if (a.pclk) {
+      __syncthreads();
+      if (tid == 0) atomicAdd(&a.pclk[15], wall_clock64() - tl);
+    }
   });
   if (over) atomicOr(a.err, ERR_INBOUND);
 }
@@ -1168,7 +1187,10 @@ __device__ inline void mv_after_consume(const MvArgs& a, uint32_t q, uint32_t me
 // (records compacted by ballot, sorted across lanes), > wave_c by one lane.
 __global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void k_mv_consume(MvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t f = mv_xcd_bin(blockIdx.x, a.fno);  // local kept-bin index
+  // (local kept-bin index, in dispatch order: stakes fall with node id, so the low bins
+  // hold the hubs' long lists; contiguous ranges per XCD left XCD 0 the heavy bins, C5's
+  // gather 5.70 vs 4.41 ms per round)
+  const uint32_t f = blockIdx.x;
   if (f >= a.fno) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, BP = 1u << a.BSF, Sg = a.Sg, v0 = (a.flo + f) << a.BSF;
   if (v0 >= a.vhi) return;
@@ -1567,7 +1589,7 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     e.mv_attr_set = true;
   }
   const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8;
-  const uint32_t ggrid = ((fno + 7) / 8) * 8;
+  const uint32_t ggrid = fno;
   const uint32_t xgrid = 2048;
   uint32_t lag = 2;
   if (const char* x = std::getenv("GS_MV_LAG")) lag = std::max<uint32_t>(1, (uint32_t)std::strtoul(x, nullptr, 10));
