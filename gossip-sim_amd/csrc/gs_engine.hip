@@ -955,6 +955,23 @@ int gs_read_caches(gs_engine* eh, uint32_t slot, uint32_t* up, uint32_t* len, ui
   return GS_OK;
 }
 
+// n elements of elem bytes, stride bytes apart, device -> host: one contiguous copy per
+// chunk of 2^20 elements, picked on the host (a 2D copy of 1- or 4-byte rows runs row by
+// row: minutes at 10M nodes).
+static hipError_t strided_d2h(Engine* e, void* dst, const void* src, size_t elem, size_t stride, size_t n) {
+  const size_t CH = (size_t)1 << 20;
+  std::vector<uint8_t> tmp;
+  for (size_t i0 = 0; i0 < n; i0 += CH) {
+    const size_t c = std::min(CH, n - i0), span = (c - 1) * stride + elem;
+    tmp.resize(span);
+    hipError_t r = hipMemcpyAsync(tmp.data(), (const uint8_t*)src + i0 * stride, span, hipMemcpyDeviceToHost, e->st);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->st);
+    if (r != hipSuccess) return r;
+    for (size_t i = 0; i < c; ++i) std::memcpy((uint8_t*)dst + (i0 + i) * elem, tmp.data() + i * stride, elem);
+  }
+  return hipSuccess;
+}
+
 int gs_read_pruned_all(gs_engine* eh, uint32_t slot, uint32_t* fifo_mask) {
   ENGINE(eh);
   if (int s_ = flush_rot_clear(e)) return s_;
@@ -967,7 +984,7 @@ int gs_read_pruned_all(gs_engine* eh, uint32_t slot, uint32_t* fifo_mask) {
   if (e->msu == 1) {
     HIPC(hipMemcpyAsync(m.data(), e->mask + slot * e->mso, N * 4, hipMemcpyDeviceToHost, e->st));
   } else {
-    HIPC(hipMemcpy2DAsync(m.data(), 4, e->mask + slot * e->mso, e->msu * 4, 4, N, hipMemcpyDeviceToHost, e->st));
+    HIPC(strided_d2h(e, m.data(), e->mask + slot * e->mso, 4, e->msu * 4, N));
   }
   HIPC(hipMemcpyAsync(b.data(), e->bucket, N, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpyAsync(hl.data(), e->hl, N * NB * 2, hipMemcpyDeviceToHost, e->st));
@@ -993,7 +1010,7 @@ int gs_read_counters(gs_engine* eh, uint32_t slot, uint32_t* egress, uint32_t* i
   if (e->esu == 1) {
     HIPC(hipMemcpyAsync(eg.data(), e->egress + slot * e->eso, N, hipMemcpyDeviceToHost, e->st));
   } else {
-    HIPC(hipMemcpy2DAsync(eg.data(), 1, e->egress + slot * e->eso, e->esu, 1, N, hipMemcpyDeviceToHost, e->st));
+    HIPC(strided_d2h(e, eg.data(), e->egress + slot * e->eso, 1, e->esu, N));
   }
   HIPC(hipMemcpyAsync(hp.data(), e->hops + base, N, hipMemcpyDeviceToHost, e->st));
   HIPC(hipMemcpyAsync(pr.data(), e->prune_round + base, N, hipMemcpyDeviceToHost, e->st));
