@@ -67,6 +67,7 @@ __device__ inline void cache_update_lane(uint32_t* __restrict__ ckey, size_t PAI
   const uint32_t wl = active_max<7>(len);
   if (wc <= 4) cache_match<4>(ckey, PAIRS, q, rid, len, wl, kc0, pr, idx0, idx1, w0, w1);
   else if (wc <= 8) cache_match<8>(ckey, PAIRS, q, rid, len, wl, kc0, pr, idx0, idx1, w0, w1);
+  else if (wc <= 12) cache_match<12>(ckey, PAIRS, q, rid, len, wl, kc0, pr, idx0, idx1, w0, w1);
   else cache_match<16>(ckey, PAIRS, q, rid, len, wl, kc0, pr, idx0, idx1, w0, w1);
   up = up < 255 ? up + 1 : 255;  // rank 0 (received_cache.rs:84-86)
 #pragma unroll
@@ -90,10 +91,12 @@ __device__ inline void cache_update_lane(uint32_t* __restrict__ ckey, size_t PAI
     }
 }
 
-// Sorts rk[0..16) ascending with the narrowest network that covers wc keys.
+// Sorts rk[0..16) ascending with the narrowest network that covers wc keys (rk[wc..16)
+// are ~0). (C5's waves: the largest in-degree of 64 lanes averages 12.5.)
 __device__ inline void sort_ranked(uint32_t (&rk)[16], uint32_t wc) {
   if (wc <= 4) sort_net<4>(rk);
   else if (wc <= 8) sort_net<8>(rk);
+  else if (wc <= 12) sort_net<16, 16, 12>(rk);
   else sort_net<16>(rk);
 }
 

@@ -279,10 +279,12 @@ __device__ inline void cswap(uint32_t& x, uint32_t& y) {
 }
 
 // Batcher odd-even merge sort of r[0, NS) (NS a power of two), register-resident:
-// 63 comparators for 16 keys, 191 for 32.
-template <int NS, int M>
+// 63 comparators for 16 keys, 191 for 32. W < NS: r[W, NS) hold ~0 (the largest key), which
+// no comparator moves, so the comparators reaching past W are dropped (the first W keys
+// are sorted with fewer).
+template <int NS, int M, int W = NS>
 __device__ inline void sort_net(uint32_t (&r)[M]) {
-  static_assert(NS <= M && (NS & (NS - 1)) == 0, "power-of-two prefix");
+  static_assert(NS <= M && (NS & (NS - 1)) == 0 && W <= NS, "power-of-two prefix");
 #pragma unroll
   for (int p = 1; p < NS; p <<= 1)
 #pragma unroll
@@ -291,7 +293,7 @@ __device__ inline void sort_net(uint32_t (&r)[M]) {
       for (int j = k % p; j + k < NS; j += 2 * k)
 #pragma unroll
         for (int i = 0; i < k; ++i)
-          if (i + j + k < NS && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cswap(r[i + j], r[i + j + k]);
+          if (i + j + k < W && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cswap(r[i + j], r[i + j + k]);
 }
 __device__ inline void sort16(uint32_t (&r)[16]) { sort_net<16>(r); }
 

@@ -229,6 +229,7 @@ __device__ inline void consume_lane(const RoundArgs& a, size_t p, const uint16_t
   // records beyond wc are 0xFFFFFFFF already, so sorting the first 4/8/16 suffices
   if (wc <= 4) sort_net<4>(rk);
   else if (wc <= 8) sort_net<8>(rk);
+  else if (wc <= 12) sort_net<16, 16, 12>(rk);
   else sort_net<16>(rk);
   // ids of ranks 2h, 2h + 1 in one register (padding ranks carry 0xFFFF, which no key
   // below equals: ids are < N <= 65,535 and an unused row reads as 0xFFFF)
