@@ -65,7 +65,7 @@ struct MvArgs {
   const uint8_t* fk;      // [S] failure class index of the slot's count (0: no failures)
   const uint32_t* origin;
   const uint32_t* mask;   // node-major [N][SP]
-  const uint32_t* gt;     // this group's table (GT_WORDS words)
+  const uint32_t* gt;     // this group's table (GT_STRIDE words)
   uint8_t* hops;
   uint32_t* cnt;
   uint32_t* inb;
@@ -142,6 +142,38 @@ __host__ __device__ inline size_t mv_hist_bytes(uint32_t nbins) { return 4 * (si
 // --------------------------------------------------------------- expand ----
 constexpr uint32_t MV_SG4 = 7;  // slot quads per group (GW <= 28)
 
+__host__ __device__ inline uint32_t mv_ohash(uint32_t x) { return (x * 0x9E3779B1u) >> 25; }
+
+// The group's slots as the expand reads them (LDS): origins, failure classes, the slots
+// with no failures (fz; 0 when the origin hash is incomplete, so that every slot takes
+// the per-slot path), and the origin -> slot-mask hash of the group table.
+struct MvSlots {
+  uint32_t sorg[32], sfk[32];
+  uint2 otab[128];
+  uint32_t fz;
+};
+
+// (no barrier: the caller's first __syncthreads publishes S)
+__device__ inline void mv_slots_load(const MvArgs& a, MvSlots& S, uint32_t tid, uint32_t nth) {
+  if (tid < a.Sg) {
+    S.sorg[tid] = a.origin[a.s0 + tid];
+    S.sfk[tid] = a.fk[a.s0 + tid];
+  }
+  const uint2* ot = reinterpret_cast<const uint2*>(a.gt + GT_OT);
+  for (uint32_t i = tid; i < 128; i += nth) S.otab[i] = ot[i];
+  if (tid < 64) {  // wave 0 (every kernel has >= 256 threads)
+    const uint64_t z = __ballot(tid < a.Sg && a.fk[a.s0 + tid] == 0);
+    if (tid == 0) S.fz = a.gt[GT_OTOK] ? (uint32_t)z : 0u;
+  }
+}
+
+// The group's slots whose origin is node x.
+__device__ inline uint32_t mv_origin_slots(const MvSlots& S, uint32_t x) {
+  const uint32_t h0 = mv_ohash(x);
+  const uint2 e0 = S.otab[h0], e1 = S.otab[(h0 + 1) & 127u];
+  return (e0.x == x ? e0.y : 0u) | (e1.x == x ? e1.y : 0u);
+}
+
 // Words of an own-bucket row in the multi-source BFS: the ring, hl | bucket << 16, the
 // peers' failure classes (one byte each), padded to 16 bytes.
 template <int ASZP>
@@ -150,11 +182,16 @@ constexpr int mv_orw() { return ((ASZP + 1 + ASZP / 4) + 3) & ~3; }
 // One frontier entry (node u, entry k, slot mask M): the pushed-to ring slots of every
 // slot in M (PushActiveSet::get_nodes(..).take(fanout), gossip.rs:527-541: unpruned,
 // not the origin, failed peers burn their slot) as per-ring-slot slot masks acc[s], and
-// each slot's egress byte. Slots whose mask is empty, that have no failures and share
-// the group's first origin push the same set: it is computed once.
+// each slot's egress byte.
+// Plain slots (no prunes at u, no failures) push to the first `fanout` ring positions
+// except their own origin: one prefix of the ring for all of them, and a slot whose
+// origin sits in that prefix swaps it for position `fanout` (the group's origins are
+// looked up once per pushed-to peer in an LDS hash). Only the other slots run the
+// per-slot selection, which a wave executes for the union of its lanes' slots (round 4;
+// before, every slot of M ran it unless it shared the group's first origin).
 template <int ASZP>
-__device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const uint32_t* sorg, const uint32_t* sfk,
-                                       uint32_t (&row)[ASZP], uint32_t (&acc)[ASZP], uint32_t& u) {
+__device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const MvSlots& S, uint32_t (&row)[ASZP],
+                                       uint32_t (&acc)[ASZP], uint32_t& u) {
   constexpr int TQ = (mv_orw<ASZP>() - ASZP) / 4;
   u = ent.x & 0xFFFFFFu;
   const uint32_t k = ent.x >> 24, M = ent.y;
@@ -189,9 +226,37 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const uint32_
     for (int s = 0; s < ASZP; ++s) fc[s] = a.any_fail ? a.fcls[row[s]] : 0xFFu;
   }
   const uint32_t head = hv & 0xFF, len = hv >> 8;
-  const uint32_t org0 = sorg[0];
-  uint32_t tk0 = 0, msh = 0;
-  bool have0 = false;
+  uint32_t plain = 0, ep = 0, epr = 0;
+  if constexpr (ASZP < 32) {
+    uint32_t pmz = 0;  // slots with no prunes at u
+#pragma unroll
+    for (uint32_t q = 0; q < MV_SG4; ++q)
+      pmz |= ((uint32_t)(m4[q].x == 0) | ((uint32_t)(m4[q].y == 0) << 1) | ((uint32_t)(m4[q].z == 0) << 2) |
+              ((uint32_t)(m4[q].w == 0) << 3)) << (4 * q);
+    plain = M & S.fz & pmz;
+    if (plain) {
+      const uint32_t SZ = a.ASZ, full = (1u << SZ) - 1u;
+      const uint32_t L = min(len, SZ), nf = min(L, a.fanout);
+      const uint32_t pre = (1u << nf) - 1u, nxp = L > a.fanout ? 1u << a.fanout : 0u;  // ring positions
+      const uint32_t tkn = ((pre << head) | (pre >> (SZ - head))) & full;               // physical slots
+      const uint32_t nxt = ((nxp << head) | (nxp >> (SZ - head))) & full;
+      uint32_t rem = 0;  // plain slots whose origin is in the prefix
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        if (!((tkn >> s) & 1u)) continue;
+        const uint32_t om = mv_origin_slots(S, row[s]) & plain;
+        acc[s] |= plain & ~om;
+        rem |= om;
+      }
+      if (rem) {
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s)
+          if ((nxt >> s) & 1u) acc[s] |= rem;
+      }
+      ep = (uint32_t)__popc(tkn);
+      epr = nxt ? 0u : rem;  // (no position `fanout`: those slots push one fewer)
+    }
+  }
   const bool own_u = u - a.vlo < a.vhi - a.vlo;  // egress is kept for owned nodes
   uint8_t* eg = a.egress + (size_t)(u - a.vlo) * a.SP + a.s0;
 #pragma unroll
@@ -204,26 +269,20 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const uint32_
     for (uint32_t t = 0; t < 4; ++t) {
       const uint32_t j = 4 * q + t;
       if (!((mq4 >> t) & 1u)) continue;
-      const uint32_t pm = t == 0 ? m4[q].x : t == 1 ? m4[q].y : t == 2 ? m4[q].z : m4[q].w;
-      const uint32_t f = sfk[j];
-      uint32_t tk;
-      if (pm == 0 && f == 0 && sorg[j] == org0) {  // the shared push set
-        if (!have0) {
-          tk0 = taken_slots<ASZP>(row, head, len, a.ASZ, 0u, org0, a.fanout);
-          have0 = true;
-        }
-        tk = tk0;
-        msh |= 1u << j;
-      } else {
-        tk = taken_slots<ASZP>(row, head, len, a.ASZ, pm, sorg[j], a.fanout);
-        if (f) {  // failed peers burn their fanout slot (gossip.rs:538-541)
-#pragma unroll
-          for (int s = 0; s < ASZP; ++s)
-            if (fc[s] <= f) tk &= ~(1u << s);
-        }
-#pragma unroll
-        for (int s = 0; s < ASZP; ++s) acc[s] |= ((tk >> s) & 1u) << j;
+      if ((plain >> j) & 1u) {
+        egw |= (ep - ((epr >> j) & 1u)) << (8 * t);
+        continue;
       }
+      const uint32_t pm = t == 0 ? m4[q].x : t == 1 ? m4[q].y : t == 2 ? m4[q].z : m4[q].w;
+      const uint32_t f = S.sfk[j];
+      uint32_t tk = taken_slots<ASZP>(row, head, len, a.ASZ, pm, S.sorg[j], a.fanout);
+      if (f) {  // failed peers burn their fanout slot (gossip.rs:538-541)
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s)
+          if (fc[s] <= f) tk &= ~(1u << s);
+      }
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) acc[s] |= ((tk >> s) & 1u) << j;
       egw |= (uint32_t)__popc(tk) << (8 * t);
     }
     if (!own_u) {
@@ -234,11 +293,6 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const uint32_
       for (uint32_t t = 0; t < 4; ++t)
         if ((mq4 >> t) & 1u) eg[4 * q + t] = (uint8_t)(egw >> (8 * t));
     }
-  }
-  if (msh) {
-#pragma unroll
-    for (int s = 0; s < ASZP; ++s)
-      if ((tk0 >> s) & 1u) acc[s] |= msh;
   }
 }
 
@@ -253,7 +307,8 @@ template <int ASZP, uint32_t XT>
 __global__ __launch_bounds__(XT) void k_mv_expand(MvArgs a, uint32_t d, uint32_t pi, const uint2* __restrict__ q0,
                                                   const uint2* __restrict__ q1) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t sorg[32], sfk[32], sbase;
+  __shared__ MvSlots S;
+  __shared__ uint32_t sbase;
   if (pi != MV_NOPAIR) d = a.dpair[pi];
   const uint32_t qn = d < 254 ? a.lvl[d] : 0u;
   const uint2* __restrict__ qcur = (d & 1) ? q1 : q0;
@@ -266,10 +321,7 @@ __global__ __launch_bounds__(XT) void k_mv_expand(MvArgs a, uint32_t d, uint32_t
     return;
   }
   const uint32_t tid = threadIdx.x, nb = a.nbc, BSC = a.BSC, UB = a.UB, BPm = (1u << BSC) - 1;
-  if (tid < a.Sg) {
-    sorg[tid] = a.origin[a.s0 + tid];
-    sfk[tid] = a.fk[a.s0 + tid];
-  }
+  mv_slots_load(a, S, tid, XT);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);  // [nb] + scan words
   unsigned long long* stage = reinterpret_cast<unsigned long long*>(smem + mv_hist_bytes(nb));  // [XT * ASZP]
   for (uint32_t w = blockIdx.x; w < G; w += gridDim.x) {
@@ -279,7 +331,7 @@ __global__ __launch_bounds__(XT) void k_mv_expand(MvArgs a, uint32_t d, uint32_t
 #pragma unroll
     for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
     const uint32_t i = w * XT + tid;
-    if (i < qn) mv_expand_entry<ASZP>(a, qcur[i], sorg, sfk, row, acc, u);
+    if (i < qn) mv_expand_entry<ASZP>(a, qcur[i], S, row, acc, u);
     // every LDS atomic after every load: each record's rank within its coarse bin
     uint32_t rk[ASZP];
 #pragma unroll
@@ -522,13 +574,11 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
   // global fills are written once at the end
   extern __shared__ __attribute__((aligned(16))) uint32_t lp[];
   __shared__ uint2 qL[2][MV_SQ];
-  __shared__ uint32_t sorg[32], sfk[32], gt[GT_WORDS], cnt_s;
+  __shared__ MvSlots S;
+  __shared__ uint32_t gt[GT_WORDS], cnt_s;
   const uint32_t tid = threadIdx.x;
   const bool LP = a.fno <= MV_SMALL_LP;  // (uniform; beyond, device-scope atomics on a.pused)
-  if (tid < a.Sg) {
-    sorg[tid] = a.origin[a.s0 + tid];
-    sfk[tid] = a.fk[a.s0 + tid];
-  }
+  mv_slots_load(a, S, tid, MV_ST);
   for (uint32_t i = tid; i < GT_WORDS; i += MV_ST) gt[i] = a.gt[i];
   uint32_t d = mode == MV_TAIL ? a.dpair[pi] : d0;
   bool inL = false;  // the current level's entries [0, MV_SQ) are in qL[d & 1]
@@ -578,7 +628,7 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
       uint32_t row[ASZP], acc[ASZP], u = 0;
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
-      if (i < qn) mv_expand_entry<ASZP>(a, inL && i < MV_SQ ? ql[i] : qg[i], sorg, sfk, row, acc, u);
+      if (i < qn) mv_expand_entry<ASZP>(a, inL && i < MV_SQ ? ql[i] : qg[i], S, row, acc, u);
       if (a.pclk && i0 == 0) {  // (profiling only: wait for the entry's loads)
         uint32_t x = 0;
 #pragma unroll
@@ -729,13 +779,11 @@ __global__ __launch_bounds__(MV_PT, 4) void k_mv_levels(MvArgs a, uint32_t mode,
                                                      uint2* __restrict__ q0, uint2* __restrict__ q1,
                                                      uint32_t* __restrict__ hstate, const uint2* __restrict__ seeds,
                                                      uint32_t nseed, uint32_t seq, uint32_t* __restrict__ bar) {
-  __shared__ uint32_t sorg[32], sfk[32], gt[GT_WORDS], s_base, s_qn;
+  __shared__ MvSlots S;
+  __shared__ uint32_t gt[GT_WORDS], s_base, s_qn;
   const uint32_t tid = threadIdx.x, G = gridDim.x, lane = tid & 63;
   const uint32_t gtid = blockIdx.x * MV_PT + tid, GT = G * MV_PT;
-  if (tid < a.Sg) {
-    sorg[tid] = a.origin[a.s0 + tid];
-    sfk[tid] = a.fk[a.s0 + tid];
-  }
+  mv_slots_load(a, S, tid, MV_PT);
   for (uint32_t i = tid; i < GT_WORDS; i += MV_PT) gt[i] = a.gt[i];
   if (tid == 0) s_base = __hip_atomic_load(&bar[160], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // GS_PHASE_PROFILE: clocks of workgroup 0's thread 0 at pclk[5..8] (setup, the first
@@ -780,7 +828,7 @@ __global__ __launch_bounds__(MV_PT, 4) void k_mv_levels(MvArgs a, uint32_t mode,
       uint32_t row[ASZP], acc[ASZP], u = 0;
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
-      if (i < qn) mv_expand_entry<ASZP>(a, mv_q_load(&qc[i]), sorg, sfk, row, acc, u);
+      if (i < qn) mv_expand_entry<ASZP>(a, mv_q_load(&qc[i]), S, row, acc, u);
       if (clk && i0 == wbase) {  // (profiling only: wait for the entry's loads)
         uint32_t x = 0;
 #pragma unroll
@@ -1339,12 +1387,26 @@ void mv_build_groups(Engine& e, const std::vector<uint32_t>& origins, const std:
                      const std::vector<uint8_t>& bucket, std::vector<uint32_t>& gtab, std::vector<uint2>& seeds) {
   const uint32_t GW = e.mv.GW;
   const uint32_t ng = (e.S + GW - 1) / GW;
-  gtab.assign((size_t)ng * GT_WORDS, 0);
+  gtab.assign((size_t)ng * GT_STRIDE, 0);
   seeds.clear();
   e.mv_groups.clear();
   for (uint32_t g = 0; g < ng; ++g) {
     const uint32_t s0 = g * GW, sg = std::min(GW, e.S - s0);
-    uint32_t* t = gtab.data() + (size_t)g * GT_WORDS;
+    uint32_t* t = gtab.data() + (size_t)g * GT_STRIDE;
+    {  // origin -> slot mask, open addressing with two probes (mv_origin_slots)
+      uint32_t* ot = t + GT_OT;
+      for (uint32_t i = 0; i < 128; ++i) ot[2 * i] = 0xFFFFFFFFu;
+      bool ok = true;
+      for (uint32_t j = 0; j < sg; ++j) {
+        const uint32_t o = origins[s0 + j], h0 = mv_ohash(o), h1 = (h0 + 1) & 127u;
+        const uint32_t h = (ot[2 * h0] == o || ot[2 * h0] == 0xFFFFFFFFu) ? h0
+                           : (ot[2 * h1] == o || ot[2 * h1] == 0xFFFFFFFFu) ? h1 : 128u;
+        if (h == 128u) { ok = false; continue; }
+        ot[2 * h] = o;
+        ot[2 * h + 1] |= 1u << j;
+      }
+      t[GT_OTOK] = ok ? 1u : 0u;
+    }
     for (uint32_t k = 0; k < (uint32_t)NB; ++k)
       for (uint32_t j = 0; j < sg; ++j)
         if (obkt[s0 + j] >= k) t[GT_OWN + k] |= 1u << j;
@@ -1398,7 +1460,7 @@ hipError_t mv_update_failures(Engine& e, const std::vector<uint32_t>& nf) {
 static MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   MvArgs a;
   a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.own = e.own; a.fcls = e.mv_fcls; a.fk = e.mv_fk;
-  a.origin = e.origin; a.mask = e.mask; a.gt = e.mv_gtab + (size_t)g * GT_WORDS;
+  a.origin = e.origin; a.mask = e.mask; a.gt = e.mv_gtab + (size_t)g * GT_STRIDE;
   a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb; a.egress = e.egress; a.err = e.err;
   a.vis = e.mv_vis; a.lvl = e.lvl; a.hlvl = e.mv_hlvl_dev; a.T = e.mv_T; a.area = e.mv_area; a.ctr = e.mv_ctr;
   a.dpair = e.mv_dpair; a.hprof = nullptr;

@@ -377,7 +377,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     ALLOC(e->mv_fcls, N, 0xFF);
     ALLOC(e->mv_fk, S, 0);
     ALLOC(e->mv_thr, S, 0);
-    ALLOC(e->mv_gtab, (size_t)((S + g.GW - 1) / g.GW) * GT_WORDS, 0);
+    ALLOC(e->mv_gtab, (size_t)((S + g.GW - 1) / g.GW) * GT_STRIDE, 0);
     ALLOC(e->mv_seed, S, 0);
   }
   e->h_nfail_any.assign(S, 0);

@@ -33,7 +33,10 @@ struct BinGeom {
 // Geometry of the multi-source frontier BFS (gs_bfs_multi.hip): bins of 2^BS nodes,
 // level records u64 = src | node-in-coarse-bin << UB | slot mask << (UB + BSC); pool records
 // src | node-in-fine-bin << UB | hop << (UB + BSF) | slot mask << (UB + BSF + 8); slot groups of <= GW.
-constexpr uint32_t GT_WORDS = 96;  // per-group table words
+constexpr uint32_t GT_WORDS = 96;  // per-group table words (the part the level kernels copy to LDS)
+// ... followed by the group's origin -> slot-mask hash (128 (id, mask) pairs, two probes;
+// word GT_OTOK of the table = 1 when every origin is in it): a group's table is GT_STRIDE words
+constexpr uint32_t GT_OT = GT_WORDS, GT_OTOK = 94, GT_STRIDE = GT_WORDS + 256;
 struct MvGeom {
   uint32_t UB = 0, BSC = 0, BSF = 0, nbc = 0, nbf = 0, GW = 0, TW = 0, gcap = 0, gcap_c = 0;
   uint32_t XT = 256;  // frontier entries per expand slice (256, or 1,024 for wide T rows)
@@ -130,7 +133,7 @@ struct Engine {
   std::vector<std::vector<uint32_t>> mv_pred;  // per group: the last known level sizes (empty: none yet)
   std::vector<uint32_t> mv_prof_seen;          // per group: the profile sequence number last read
   uint32_t mv_seq = 0;                         // profile sequence numbers handed to the tail kernels
-  uint32_t* mv_gtab = nullptr;    // [groups][GT_WORDS]
+  uint32_t* mv_gtab = nullptr;    // [groups][GT_STRIDE]
   uint2* mv_seed = nullptr;       // [S] seed entries (distinct origins) of every group
   std::vector<MvGroup> mv_groups;
   bool mv_attr_set = false;
