@@ -248,7 +248,8 @@ def gather_phases(eng):
     names = {12: "count_scan", 13: "range_place", 11: "body_all", 14: "body_light", 15: "body_heavy",
              0: "small_setup", 1: "small_expand_loads", 2: "small_atomics_places", 3: "small_lt_barrier",
              4: "small_levels_e-5", 5: "lv_setup", 6: "lv_loads", 7: "lv_atomics_stores", 8: "lv_barrier",
-             9: "lv_levels_e-5", 10: "pool_records"}
+             9: "lv_levels_e-5", 10: "pool_records",
+             16: "apply_tcol_scan", 17: "apply_vis_load", 18: "apply_records", 19: "apply_tail"}
     return {nm: round(eng.kernel_time("phase." + chr(65 + i))[0], 2) for i, nm in names.items()}
 
 

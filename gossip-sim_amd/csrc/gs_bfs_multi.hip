@@ -420,6 +420,15 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
   const uint32_t tid = threadIdx.x, BSC = a.BSC, UB = a.UB, BP = 1u << BSC, BPm = BP - 1;
   const uint32_t G = (qn + a.XT - 1) / a.XT;
   const uint32_t v0 = c << BSC, nv = min(BP, a.N - v0);
+  // GS_PHASE_PROFILE: thread 0's clocks at pclk[16..19] (T column + scan, vis load, records, tail)
+  unsigned long long tm = a.pclk && tid == 0 ? wall_clock64() : 0;
+  auto mark = [&](int ph) {
+    if (a.pclk && tid == 0) {
+      const unsigned long long now = wall_clock64();
+      atomicAdd(&a.pclk[ph], now - tm);
+      tm = now;
+    }
+  };
   uint32_t* pre = reinterpret_cast<uint32_t*>(smem);  // [MV_SEG + 1]
   uint32_t* sb = pre + MV_SEG + 1;                    // [MV_SEG]
   uint32_t* visL = sb + MV_SEG;                       // [BP]
@@ -446,6 +455,7 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
     }
     __syncthreads();
     const uint32_t ct = mv_block_scan(pre, gc, ctl);
+    mark(16);
     if (ct == 0) continue;  // (uniform)
     if (tid == 0) pre[gc] = ct;
     if (!loaded) {
@@ -458,6 +468,7 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
       loaded = true;
     }
     __syncthreads();
+    mark(17);
     // MV_AR records per thread per trip: their searches and area loads are issued
     // together, so a trip waits for one memory round trip, not MV_AR
     constexpr uint32_t MV_AR = 4;
@@ -492,6 +503,7 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
       }
     }
     __syncthreads();
+    mark(18);
   }
   __syncthreads();
   if (tid < NF && f0 + tid - a.flo < a.fno) {  // each kept fine bin's pool fill
@@ -501,7 +513,10 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
     if (over) atomicOr(a.err, ERR_MV_CAP | ERR_MVD_POOL);
     if (n) a.pused[fl] = over ? (uint32_t)a.pcap : used + n;
   }
-  if (!loaded) return;  // no records: no first arrivals in this bin
+  if (!loaded) {  // no records: no first arrivals in this bin
+    mark(19);
+    return;
+  }
   // first arrivals (hop d + 1) become next-level entries, in node order
   uint32_t cntp = 0;
   for (uint32_t i = tid; i < nv; i += MV_AT) {
@@ -516,7 +531,10 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
     if (k < (tid >> 6)) off += ctl[8 + k];
     tnew += ctl[8 + k];
   }
-  if (tnew == 0) return;
+  if (tnew == 0) {
+    mark(19);
+    return;
+  }
   if (tid == 0) {
     const uint32_t base = atomicAdd(&a.lvl[d + 1], tnew);
     ctl[1] = base;
@@ -532,6 +550,7 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
     a.vis[v] = visL[i];
     pos += mv_parts(gt, v, nw, a.bucket[v], qnxt, pos);
   }
+  mark(19);
 }
 
 // ------------------------------------------------------------ small levels ----
@@ -1353,6 +1372,8 @@ void mv_geometry(uint32_t N, uint32_t S, uint32_t ASZ, uint32_t ASZP, MvGeom& g)
   (void)ASZP;
   g.UB = std::max(1u, ceil_log2(N));
   g.BSC = std::min(13u, std::max(6u, g.UB > 8 ? g.UB - 8 : 0u));   // ~256 coarse bins
+  if (const char* x = std::getenv("GS_MV_BSC"))  // (tuning: at C5, 12 and 11 lose to 13)
+    g.BSC = std::min(13u, std::max(6u, (uint32_t)std::strtoul(x, nullptr, 10)));
   g.BSF = std::min(g.BSC, 9u);  // fine bins of <= 512 nodes (gather at C4: 301 vs 412 us with 1,024)
   // (GS_MV_BSF: tuning; at most 10 so that a partition range of whole 1,024-id bins is whole fine bins)
   if (const char* x = std::getenv("GS_MV_BSF")) g.BSF = std::min(std::min(g.BSC, 10u), std::max(6u, (uint32_t)std::strtoul(x, nullptr, 10)));

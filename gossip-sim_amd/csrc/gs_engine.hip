@@ -405,7 +405,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     ALLOC(e->part_cnt, 1, 0);
     ALLOC(e->part_stats, part_stats_words(*e), 0);
   }
-  if (const char* pp = std::getenv("GS_PHASE_PROFILE"); pp && pp[0] == '1') ALLOC(e->phase_clk, 16, 0);
+  if (const char* pp = std::getenv("GS_PHASE_PROFILE"); pp && pp[0] == '1') ALLOC(e->phase_clk, 32, 0);
 
   // stakes, buckets and the static rotation prefix sums
   std::vector<uint8_t> b(N);
@@ -1088,8 +1088,8 @@ int gs_kernel_time(gs_engine* eh, const char* family, double* ms, uint64_t* laun
     *ms = 0;
     *launches = 0;
     const int ph = family[6] - 'A';
-    if (!e->phase_clk || ph < 0 || ph >= 16) return GS_OK;
-    unsigned long long v[16];
+    if (!e->phase_clk || ph < 0 || ph >= 32) return GS_OK;
+    unsigned long long v[32];
     HIPC(hipMemcpy(v, e->phase_clk, sizeof(v), hipMemcpyDeviceToHost));
     *ms = (double)v[ph] * 1e-5;
     *launches = e->timers["round"].n;
@@ -1123,7 +1123,7 @@ int gs_kernel_time_reset(gs_engine* eh) {
     kv.second.ms = 0;
     kv.second.n = 0;
   }
-  if (e->phase_clk) HIPC(hipMemsetAsync(e->phase_clk, 0, 128, e->st));
+  if (e->phase_clk) HIPC(hipMemsetAsync(e->phase_clk, 0, 256, e->st));
   return GS_OK;
 }
 
