@@ -241,9 +241,11 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     e->vlo = lo;
     e->PAIRS = (size_t)e->NP * n_slots;
   }
-  if (mode == GS_BFS_AUTO)  // measured: MULTI 2.6 vs BINNED 3.6 ms per C4 round (13 slots); BINNED ahead at 1 slot
-    mode = (n <= 8192 && n_slots >= 64) ? GS_BFS_WORKGROUP
-           : (mv_ok && n_slots >= 4)    ? GS_BFS_MULTI
+  // AUTO, measured: MULTI 2.6 vs BINNED 3.6 ms per C4 round (13 slots); BINNED ahead at 1
+  // slot; at 10M nodes (1,024-entry expand slices) MULTI already wins at 2 slots (4.86 vs 5.26 ms)
+  if (mode == GS_BFS_AUTO)
+    mode = (n <= 8192 && n_slots >= 64)                                      ? GS_BFS_WORKGROUP
+           : (mv_ok && (n_slots >= 4 || (n_slots >= 2 && e->mv.XT > 256))) ? GS_BFS_MULTI
            : bin_ok                     ? GS_BFS_BINNED
                                         : GS_BFS_LEVEL;
   if (mode == GS_BFS_BINNED && !bin_ok) {

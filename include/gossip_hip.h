@@ -53,8 +53,8 @@ enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24
  * bin); MULTI = batched multi-source frontier BFS (a frontier entry is a node and
  * the mask of slots reaching it at that level: one row expansion and one record
  * per pushed-to peer serve every such slot; large clusters). AUTO picks
- * WORKGROUP (n <= 8,192 and >= 64 slots), else MULTI (>= 4 slots), else BINNED,
- * else LEVEL. */
+ * WORKGROUP (n <= 8,192 and >= 64 slots), else MULTI (>= 4 slots, or >= 2 slots
+ * on graphs of >= 512 coarse bins: ~4M nodes and up), else BINNED, else LEVEL. */
 enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2, GS_BFS_BINNED = 3, GS_BFS_MULTI = 4 };
 enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4, GS_FLAG_BINNED_ALL_LEVELS = 8,
        GS_FLAG_WIDE_RECORDS = 16, GS_FLAG_NO_SMALL_LEVELS = 32, GS_FLAG_MISPREDICT_LEVELS = 64 };
