@@ -793,9 +793,14 @@ struct StatsArgs {
 // FULL: the step-wise gs_record_round (reads the per-round counters of every pair);
 // LITE: after a fused round whose kernels already accumulated egress/ingress/prunes
 // (EG: the BFS left egress to this pass: the multi-source BFS).
+// Grid (slots, node blocks); a block takes SP_UN x 256 nodes per trip, their loads issued
+// together: a thread's trip is a chain of dependent loads (hop, then egress and the
+// accumulators), and one node per trip left the pass bound by loads in flight (C5: 16 x
+// 10M pairs in ~0.7 ms).
+constexpr uint32_t SP_UN = 4;
 template <bool FULL, bool EG = false>
 __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
-  const uint32_t o = blockIdx.y;
+  const uint32_t o = blockIdx.x, bx = blockIdx.y, gxn = gridDim.y;
   const size_t base = (size_t)o * a.NP - a.vlo;
   const uint32_t nf = a.nfail[o];
   __shared__ uint32_t h[256];
@@ -807,25 +812,40 @@ __global__ __launch_bounds__(256) void k_stats_pass(StatsArgs a) {
   __syncthreads();
   uint32_t vis = 0, pushes = 0, sc = 0;
   uint64_t ss = 0;
-  for (uint32_t v = a.lo + blockIdx.x * blockDim.x + threadIdx.x; v < a.hi; v += gridDim.x * blockDim.x) {
-    const size_t p = base + v;
-    const uint32_t hh = a.hops[p];
-    const uint32_t c = a.cnt[p];
-    pushes += c;
-    if (FULL) {
-      a.ingress_acc[p] += c;
-      a.prune_acc[p] += a.prune_round[p];
+  constexpr uint32_t OUT = 0x1FFu;  // not a node of this pass
+  for (uint32_t vb = a.lo + bx * (SP_UN * 256); vb < a.hi; vb += gxn * (SP_UN * 256)) {
+    uint32_t hh[SP_UN], cc[SP_UN], eg[SP_UN];
+#pragma unroll
+    for (uint32_t k = 0; k < SP_UN; ++k) {
+      const uint32_t v = vb + k * 256 + threadIdx.x;
+      const bool in = v < a.hi;
+      const size_t p = base + v;
+      hh[k] = in ? a.hops[p] : OUT;
+      cc[k] = in ? a.cnt[p] : 0u;
+      eg[k] = (in && (FULL || EG)) ? a.egress[o * a.eso + (v - a.vlo) * a.esu] : 0u;
     }
-    if (hh != 0xFF) {
-      ++vis;
-      atomicAdd(&h[hh], 1u);
-      if (FULL || EG) a.egress_acc[p] += a.egress[o * a.eso + (v - a.vlo) * a.esu];
-    } else if (!(nf && a.frank[v] < nf)) {
-      a.strand[p] += 1;
-      ++sc;
-      ss += a.stake[v];
-      const uint32_t r = a.srank[v];
-      atomicOr(&a.bm[(size_t)o * a.W + (r >> 5)], 1u << (r & 31));
+#pragma unroll
+    for (uint32_t k = 0; k < SP_UN; ++k) {
+      if (hh[k] == OUT) continue;
+      const uint32_t v = vb + k * 256 + threadIdx.x;
+      const size_t p = base + v;
+      const uint32_t c = cc[k];
+      pushes += c;
+      if (FULL) {
+        a.ingress_acc[p] += c;
+        a.prune_acc[p] += a.prune_round[p];
+      }
+      if (hh[k] != 0xFF) {
+        ++vis;
+        atomicAdd(&h[hh[k]], 1u);
+        if (FULL || EG) a.egress_acc[p] += eg[k];
+      } else if (!(nf && a.frank[v] < nf)) {
+        a.strand[p] += 1;
+        ++sc;
+        ss += a.stake[v];
+        const uint32_t r = a.srank[v];
+        atomicOr(&a.bm[(size_t)o * a.W + (r >> 5)], 1u << (r & 31));
+      }
     }
   }
   atomicAdd(&acc[0], vis);
@@ -1023,10 +1043,10 @@ hipError_t launch_stats(Engine& e, uint32_t rec_slot, int mode) {
   a.lo = e.vlo;
   a.hi = e.vlo + e.NP;
   a.NP = e.NP; a.vlo = e.vlo;
-  uint32_t gx = grid_for(e.NP, 256, std::max<uint32_t>(64, 2048 / std::max<uint32_t>(e.S, 1)));
-  if (mode == 0 || mode == 3) hipLaunchKernelGGL(k_stats_pass<true>, dim3(gx, e.S), dim3(256), 0, e.st, a);
-  else if (mode == 1) hipLaunchKernelGGL(k_stats_pass<false>, dim3(gx, e.S), dim3(256), 0, e.st, a);
-  else if (mode == 4 || mode == 5) hipLaunchKernelGGL((k_stats_pass<false, true>), dim3(gx, e.S), dim3(256), 0, e.st, a);
+  uint32_t gx = grid_for(e.NP, 256 * SP_UN, std::max<uint32_t>(64, 2048 / std::max<uint32_t>(e.S, 1)));
+  if (mode == 0 || mode == 3) hipLaunchKernelGGL(k_stats_pass<true>, dim3(e.S, gx), dim3(256), 0, e.st, a);
+  else if (mode == 1) hipLaunchKernelGGL(k_stats_pass<false>, dim3(e.S, gx), dim3(256), 0, e.st, a);
+  else if (mode == 4 || mode == 5) hipLaunchKernelGGL((k_stats_pass<false, true>), dim3(e.S, gx), dim3(256), 0, e.st, a);
   if (mode != 3 && mode != 5)  // the pass only (a partition sums the partials over ranks first)
   {
     hipLaunchKernelGGL(k_bm_count, dim3(BM_CHUNKS, e.S), dim3(256), 0, e.st, e.bm, e.bm_words, e.bm_cnt);
