@@ -8,20 +8,20 @@
 #   4. the driver's window under rocprofv3 --kernel-trace --stats: the stats CSV and the
 #      window's k_round_wg launches -> profiles/r04/trace_k_round_wg_c2_r5-24.json
 #   5. the bench lines (driver window, default) that read them
-# Steps: STEPS="pmc_c2 pmc_legs sq trace bench" (default all).
+# Steps: STEPS="pmc_c2 pmc_legs sq trace trace_default bench" (default all).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/r04/${TAG:-final}
 P=profiles/r04
 mkdir -p $OUT $P
-STEPS=${STEPS:-"pmc_c2 pmc_legs sq trace bench"}
+STEPS=${STEPS:-"pmc_c2 pmc_legs sq trace trace_default bench"}
 has() { case " $STEPS " in *" $1 "*) return 0;; *) return 1;; esac; }
 # (the box's profiles/r04 is read by the later steps' bench runs; only gpurun_out/ comes back:
 # every exit copies it there)
 trap 'mkdir -p $OUT/profiles_r04 && cp -r $P/. $OUT/profiles_r04/' EXIT
 
 if has pmc_c2; then
-  for win in "5 20" "60 100"; do
+  for win in "5 20" "60 100" "20 100"; do  # (20 100: bench.py's defaults)
     set -- $win; w=$1; s=$2; tag=c2_r$w-$((w + s - 1))
     d=$OUT/pmc_$tag
     mkdir -p $d
@@ -96,6 +96,14 @@ if has trace; then
   # (c5's rounds follow c4's 25 in the same trace: c4 rounds 0-24 end at marker 24)
   python3 scripts/trace_window.py --csv $OUT/proflegs/run_kernel_trace.csv --family $MVT --marker k_mv_gather \
     --rounds 28,37 --bench-args "--only-large --legs c5" --out $P/trace_bfs_multi_c5.json || exit 1
+fi
+
+if has trace_default; then  # bench.py with no flags: rounds 20-119
+  echo "== trace default window"
+  timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $OUT/profd -o run -- \
+    python3 bench.py --steps 100 --warmup 20 --no-cpu-baseline --no-large --no-steady > $OUT/profd.log 2>&1 || { tail -20 $OUT/profd.log; exit 1; }
+  python3 scripts/trace_window.py --csv $OUT/profd/run_kernel_trace.csv --kernel k_round_wg --first 20 --count 100 \
+    --bench-args "--warmup 20 --steps 100" --out $P/trace_k_round_wg_c2_r20-119.json || exit 1
 fi
 
 if has bench; then
