@@ -88,6 +88,8 @@ def pmc_traffic(tag):
             d = json.load(f)
         src = os.path.relpath(path, ROOT)
         kh = d.get("kernel_hash")
+        if kernel_hash() is None:
+            return None, src, "no kernel hash: GS_LIB_VARIANT build or libgossip_hip.so older than its sources"
         if kh != kernel_hash():
             return None, src, f"stale: {src} measured kernels {kh}, built kernels are {kernel_hash()}"
         return d["traffic_bytes_per_launch"], src, f"PMC at kernel hash {kh}"
@@ -102,7 +104,7 @@ def trace_window(tag):
         with open(path) as f:
             d = json.load(f)
         src = os.path.relpath(path, ROOT)
-        if d.get("kernel_hash") != kernel_hash():
+        if kernel_hash() is None or d.get("kernel_hash") != kernel_hash():
             return None, f"stale: {src} traced kernels {d.get('kernel_hash')}"
         return round(d["avg_us"], 2), src
     return None, "no kernel trace of this window"

@@ -21,7 +21,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libgossip_hip.so")
 if os.environ.get("GS_LIB_VARIANT"):  # A/B builds of the same sources (scripts/), never a fallback
     LIB_PATH = os.path.join(PKG_DIR, "variants", os.environ["GS_LIB_VARIANT"], "libgossip_hip.so")
 
-GS_BFS_AUTO, GS_BFS_WORKGROUP, GS_BFS_LEVEL, GS_BFS_BINNED, GS_BFS_MULTI = 0, 1, 2, 3, 4
+GS_BFS_AUTO, GS_BFS_WORKGROUP, GS_BFS_LEVEL, GS_BFS_BINNED, GS_BFS_MULTI, GS_BFS_HYBRID = 0, 1, 2, 3, 4, 5
 GS_FLAG_PROFILE = 1
 GS_FLAG_SPLIT_ROUND = 2
 GS_FLAG_NARROW_WAVE_PATH = 4
@@ -74,6 +74,7 @@ class SimConfig(C.Structure):
 EXPORTS = {
     # name: (restype, argtypes)
     "gs_last_error": (C.c_char_p, []),
+    "gs_kernel_hash": (C.c_char_p, []),
     "gs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "gs_read_mst": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "gs_create_part": (C.c_int, [C.POINTER(Params), C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
@@ -121,6 +122,7 @@ EXPORTS = {
     "gs_kernel_time": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "gs_kernel_time_reset": (C.c_int, [C.c_void_p]),
     "gs_engine_round_kind": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "gs_engine_bfs_geometry": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     "gs_engine_memory": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "gs_engine_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_uint64)]),
@@ -136,10 +138,9 @@ EXPORTS = {
 _lib = None
 
 
-def kernel_hash():
-    """sha256 (16 hex digits) of the device sources libgossip_hip.so is built from
-    (csrc/*.hip, csrc/*.h). Profiles under profiles/ carry the hash of the kernels they
-    measured; bench.py reports a profile's figures only when it equals this one."""
+def source_hash():
+    """sha256 (16 hex digits) of the device sources on disk (csrc/*.hip, csrc/*.h), hashed
+    as gen_khash.py hashes them when the library is built."""
     import hashlib
     h = hashlib.sha256()
     d = os.path.join(PKG_DIR, "csrc")
@@ -149,6 +150,17 @@ def kernel_hash():
             with open(os.path.join(d, name), "rb") as f:
                 h.update(f.read())
     return h.hexdigest()[:16]
+
+
+def kernel_hash():
+    """The kernel hash compiled into the LOADED libgossip_hip.so (gs_kernel_hash), when it
+    equals the sources on disk; None under GS_LIB_VARIANT (an A/B build) or when the library
+    is out of date with its sources. Profiles under profiles/ carry the hash of the kernels
+    they measured; bench.py reports a profile's figures only when it equals this one."""
+    if os.environ.get("GS_LIB_VARIANT"):
+        return None
+    built = lib().gs_kernel_hash().decode()
+    return built if built == source_hash() else None
 
 
 def build(quiet=True):
@@ -242,6 +254,12 @@ class Engine:
         _check(lib().gs_engine_memory(self.h, C.byref(pb), C.byref(ob)))
         return {"n_nodes": n.value, "n_slots": s.value, "bfs_mode": m.value, "device_bytes": b.value,
                 "pair_bytes": pb.value, "other_bytes": ob.value, "fused_round": bool(f.value)}
+
+    def bfs_geometry(self):
+        """Multi / hybrid BFS geometry (diagnostics): expand slice, coarse and fine bins, group width, groups."""
+        out = np.zeros(5, dtype=np.uint32)
+        _check(lib().gs_engine_bfs_geometry(self.h, _ptr(out), 5))
+        return dict(zip(["expand_slice", "coarse_bins", "fine_bins", "group_width", "groups"], out.tolist()))
 
     def set_slots(self, origins, min_ingress=2, thresholds=0.15):
         S = self.n_slots

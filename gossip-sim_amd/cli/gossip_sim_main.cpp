@@ -90,7 +90,7 @@ void usage() {
       "  --warm-up-rounds N [200]  --influx n  --print-stats  --url URL (no RPC offline)\n"
       "engine / offline options:\n"
       "  --synthetic N        the deterministic synthetic power-law network of N nodes instead of RPC\n"
-      "  --seed S [0x5EED0003] --gpus K [1] --bfs-mode 0..3 [0 = auto]\n"
+      "  --seed S [0x5EED0003] --gpus K [1] --bfs-mode 0..5 [0 = auto; 1 workgroup, 2 level, 3 binned, 4 multi, 5 hybrid]\n"
       "  --save-results PATH  --replay-results PATH (print the report of a saved run, no GPU)\n"
       "  --influx-file PATH   write the Influx series (influx_db.rs) as line protocol to PATH\n"
       "  --influx-time-base NS  reproducible Influx timestamps NS + 1000 k (default: wall clock)\n"

@@ -75,6 +75,40 @@ static int dalloc(Engine& e, T** p, size_t count, int fill = 0) {
 
 static int flush_rot_clear(Engine* e);
 
+template <class T>
+static void dfree(Engine& e, T*& p, size_t count) {
+  if (!p) return;
+  auto it = std::find(e.allocs.begin(), e.allocs.end(), (void*)p);
+  if (it != e.allocs.end()) e.allocs.erase(it);
+  hipFree((void*)p);
+  e.dev_bytes -= std::max<size_t>(16, count * sizeof(T));
+  p = nullptr;
+}
+
+// GS_BFS_HYBRID: the push graph's T rows, level-record area and in-record regions for
+// `parts` entries per node (1 + the distinct lower origin buckets of a group; set_slots
+// grows them when a slot set needs more).
+static int hb_alloc(Engine* e, uint32_t parts) {
+  if (e->hb_pgr && parts <= e->hb_parts) return GS_OK;
+  const uint32_t old_parts = e->hb_parts;
+  hb_geometry(*e, parts);
+  const size_t area = e->mv.area_cap, pgr = (size_t)e->mv.nbc * e->hb_bin_cap, T = e->mv.rows_cap * e->mv.TW;
+  hb_geometry(*e, old_parts ? old_parts : 1);  // (unchanged until the new sizes are accepted)
+  if ((double)area > (double)0xFFFFFFF0u || (double)pgr > (double)0xFFFFFFF0u)
+    return fail(GS_ERANGE, "hybrid BFS: the push graph (nodes x active-set size x " + std::to_string(parts) +
+                               " entries per node) exceeds 2^32 records");
+  HIPC(hipStreamSynchronize(e->st));
+  dfree(*e, e->mv_T, e->mv.rows_cap * e->mv.TW);
+  dfree(*e, e->mv_area, e->mv.area_cap);
+  dfree(*e, e->hb_pgr, (size_t)e->mv.nbc * e->hb_bin_cap);
+  hb_geometry(*e, parts);
+  int st = dalloc(*e, &e->mv_T, T, 0);
+  if (!st) st = dalloc(*e, &e->mv_area, area, 0);
+  if (!st) st = dalloc(*e, &e->hb_pgr, pgr, 0);
+  if (st) e->slots_set = false;  // (no BFS runs on the missing buffers)
+  return st;
+}
+
 static void destroy_engine(Engine* e) {
   if (!e) return;
   if (e->st) hipStreamSynchronize(e->st);
@@ -131,9 +165,11 @@ static int check_err(Engine* e) {
   HIPC(hipMemcpyAsync(e->h_err, e->err, 4, hipMemcpyDeviceToHost, e->st));
   HIPC(hipStreamSynchronize(e->st));
   const uint32_t f = e->h_err[0];
-  if (f & ERR_SYNC)  // (first: a barrier that timed out leaves every later result suspect)
+  if (f & ERR_SYNC) {  // (first: a barrier that timed out leaves every later result suspect)
+    e->broken = true;  // its barrier epochs are out of step: every later call is refused
     return fail(GS_EHIP, "multi-source BFS: a grid barrier of the persistent level kernel timed out (workgroups not "
-                         "co-resident?); rerun without GS_MV_PERSIST=1");
+                         "co-resident?); the engine is unusable -- destroy it and rerun without GS_MV_PERSIST=1");
+  }
   if (f & ERR_INBOUND)
     return fail(GS_ERANGE, "inbound capacity exceeded: a node received more than " + std::to_string(e->capin) +
                                " pushes in one round; recreate the engine with a larger inbound_capacity");
@@ -219,7 +255,11 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   bin_geometry(n, pairs, e->fcap, e->bin, !(prm->flags & GS_FLAG_WIDE_RECORDS));
   const bool bin_ok = pairs <= (1ull << 28) && bin_supported(e->bin, e->fcap);
   mv_geometry(n, n_slots, e->ASZ, e->ASZP, e->mv);
-  const bool mv_ok = mv_supported(e->mv, e->ASZP);
+  // (expand slice w writes its records at w * XT * ASZ and a T row holds that place as a u32:
+  // the whole area must stay below 2^32 records -- ~16M nodes x 20-slot groups x a wide
+  // active set would not)
+  const bool mv_area_ok = (double)e->mv.rows_cap * e->mv.XT * e->ASZ <= (double)0xFFFFFFF0u;
+  const bool mv_ok = mv_supported(e->mv, e->ASZP) && mv_area_ok;
   if (part) {  // a partition rank runs the multi-source BFS over its replicated tables
     if (mode != GS_BFS_AUTO && mode != GS_BFS_MULTI) {
       destroy_engine(e);
@@ -254,25 +294,40 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   }
   if (mode == GS_BFS_MULTI && !mv_ok) {
     destroy_engine(e);
-    return fail(GS_EINVAL, "multi-source BFS: bin geometry exceeds LDS (use GS_BFS_LEVEL)");
+    return fail(GS_EINVAL, mv_area_ok ? "multi-source BFS: bin geometry exceeds LDS (use GS_BFS_LEVEL)"
+                                      : "multi-source BFS: a level's record area (frontier capacity x expand slice x "
+                                        "active-set size) exceeds 2^32 records (use GS_BFS_HYBRID or GS_BFS_LEVEL)");
   }
   if (mode == GS_BFS_WORKGROUP && (n > 65535 || lds > 160 * 1024)) {
     destroy_engine(e);
     return fail(GS_EINVAL, "workgroup BFS needs the per-slot state (9 B/node) to fit in 160 KiB of LDS");
   }
-  if (mode != GS_BFS_WORKGROUP && mode != GS_BFS_LEVEL && mode != GS_BFS_BINNED && mode != GS_BFS_MULTI) {
+  if (mode == GS_BFS_HYBRID && !mv_ok) {
+    destroy_engine(e);
+    return fail(GS_EINVAL, "hybrid BFS: bin geometry exceeds LDS (use GS_BFS_LEVEL)");
+  }
+  if (mode != GS_BFS_WORKGROUP && mode != GS_BFS_LEVEL && mode != GS_BFS_BINNED && mode != GS_BFS_MULTI &&
+      mode != GS_BFS_HYBRID) {
     destroy_engine(e);
     return fail(GS_EINVAL, "bfs_mode");
   }
   e->bfs_mode = mode;
-  e->inb_valid = mode != GS_BFS_MULTI;  // multi: no inbound rows until a step-wise BFS
+  const bool mvl = mv_layout(*e);
+  e->inb_valid = !mvl;  // multi / hybrid: no inbound rows until a BFS writes them
+  if (mode == GS_BFS_HYBRID) {  // no pool records: slot groups limited by the level records only
+    MvGeom& g = e->mv;
+    g.GW = std::min(28u, (64u - g.UB - g.BSC) & ~3u);
+    g.q_cap = (size_t)n * std::min<size_t>(std::min<size_t>(n_slots, g.GW), 26) + 64;
+    e->hb_dsp = std::min<uint32_t>(n_slots, g.GW) <= 16 ? 16u : 32u;
+    hb_geometry(*e, 1);
+  }
   // one-kernel round (gs_round): per-slot state in LDS, at most 160 KiB per workgroup
   e->fused = mode == GS_BFS_WORKGROUP && !(prm->flags & GS_FLAG_SPLIT_ROUND) &&
              round_wg_lds_bytes(n, e->fcap, e->ASZP) <= 160 * 1024;
 
   const size_t N = n, S = n_slots, PAIRS = e->PAIRS, NP = e->NP;
   e->SP = (uint32_t)((S + 3) & ~(size_t)3);
-  if (mode == GS_BFS_MULTI) {  // node-major masks / egress: a node's slots share one line
+  if (mvl) {  // node-major masks / egress: a node's slots share one line
     e->mso = 1; e->msu = e->SP; e->eso = 1; e->esu = e->SP; e->mask_words = N * e->SP;
     // node lines: when a node's own-entry row and its masks fit 128 B, both live in one
     // line of the row table (stride 32 words, masks at the row's end): an expansion
@@ -310,7 +365,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   size_t b0 = e->dev_bytes;  // per-(slot, node) state from here (a partition rank: its own nodes)
   ALLOC(e->hops, PAIRS, 0xFF);
   ALLOC(e->cnt, PAIRS, 0);
-  if (mode != GS_BFS_MULTI) ALLOC(e->inb, (size_t)e->capin * PAIRS, 0);  // multi: on first use (ensure_inb)
+  if (!mvl) ALLOC(e->inb, (size_t)e->capin * PAIRS, 0);  // multi / hybrid: on first use (ensure_inb)
   ALLOC(e->cmeta, PAIRS, 0);
   ALLOC(e->ckey, (size_t)CACHE_CAP * PAIRS, 0);
   ALLOC(e->egress, std::max(PAIRS, NP * e->esu), 0);
@@ -335,7 +390,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     ALLOC(e->bin_binoff, e->bin.nbins, 0);
     ALLOC(e->bin_vis, (size_t)e->bin.nbins << (e->bin.BS - 5), 0);  // whole bins (applies read a bin's words)
   }
-  if (mode == GS_BFS_BINNED || mode == GS_BFS_MULTI) {  // host-mapped level sizes the level loops poll
+  if (mode == GS_BFS_BINNED || mvl) {  // host-mapped level sizes the level loops poll
     if (hipHostMalloc(&e->mv_hlvl, 272 * 4, hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void**)&e->mv_hlvl_dev, e->mv_hlvl, 0) != hipSuccess) {
       destroy_engine(e);
@@ -344,7 +399,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     e->mv_hstate_dev = e->mv_hlvl_dev + 256;
     // the predicted level loops: per-pair levels, and one level profile per slot group
     ALLOC(e->mv_dpair, 258, 0);
-    const size_t ng = mode == GS_BFS_MULTI ? (S + e->mv.GW - 1) / e->mv.GW : 1;
+    const size_t ng = mvl ? (S + e->mv.GW - 1) / e->mv.GW : 1;
     if (hipHostMalloc(&e->mv_prof, ng * MV_PROF_WORDS * 4, hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void**)&e->mv_prof_dev, e->mv_prof, 0) != hipSuccess) {
       destroy_engine(e);
@@ -354,7 +409,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     e->mv_pred.assign(ng, {});
     e->mv_prof_seen.assign(ng, 0);
   }
-  if (mode == GS_BFS_MULTI) {
+  if (mvl) {
     const MvGeom& g = e->mv;
     if (const char* dg = std::getenv("GS_MV_DIAG"); dg && dg[0] == '1') e->mv_diag = true;
     if (const char* fu = std::getenv("GS_MV_FUSED"); fu && fu[0] == '1') e->mv_fused = true;
@@ -365,17 +420,24 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     ALLOC(e->mv_vis, N, 0);
     ALLOC(e->mv_q[0], g.q_cap, 0);
     ALLOC(e->mv_q[1], g.q_cap, 0);
-    ALLOC(e->mv_T, g.rows_cap * g.TW, 0);
-    ALLOC(e->mv_area, g.area_cap, 0);
     ALLOC(e->mv_ctr, 4, 0);
-    const uint32_t fno = mv_kept_bins(*e);  // a partition rank pools records to its own nodes only
-    e->part_flo = e->vlo >> g.BSF;
-    e->part_fno = fno;
-    b0 = e->dev_bytes;
-    ALLOC(e->mv_pool, (size_t)fno * g.pcap, 0);
-    ALLOC(e->mv_pused, fno, 0);
-    ALLOC(e->mv_bar, 256, 0);  // the persistent level kernel's barrier words (MV_BAR_WORDS)
-    e->pair_bytes += e->dev_bytes - b0;
+    if (mode == GS_BFS_HYBRID) {
+      ALLOC(e->hb_dist, N * e->hb_dsp, 0xFF);
+      ALLOC(e->hb_pgo, N, 0);
+      ALLOC(e->hb_F, 3 * N, 0);
+      if (int s_ = hb_alloc(e, 1)) { destroy_engine(e); return s_; }
+    } else {
+      ALLOC(e->mv_T, g.rows_cap * g.TW, 0);
+      ALLOC(e->mv_area, g.area_cap, 0);
+      const uint32_t fno = mv_kept_bins(*e);  // a partition rank pools records to its own nodes only
+      e->part_flo = e->vlo >> g.BSF;
+      e->part_fno = fno;
+      b0 = e->dev_bytes;
+      ALLOC(e->mv_pool, (size_t)fno * g.pcap, 0);
+      ALLOC(e->mv_pused, fno, 0);
+      ALLOC(e->mv_bar, 256, 0);  // the persistent level kernel's barrier words (MV_BAR_WORDS)
+      e->pair_bytes += e->dev_bytes - b0;
+    }
     ALLOC(e->mv_fcls, N, 0xFF);
     ALLOC(e->mv_fk, S, 0);
     ALLOC(e->mv_thr, S, 0);
@@ -464,9 +526,10 @@ int gs_create_part(const gs_params* prm, const uint64_t* stakes, uint32_t n, uin
 
 void gs_destroy(gs_engine* eh) { destroy_engine(reinterpret_cast<Engine*>(eh)); }
 
-#define ENGINE(eh)                                              \
-  Engine* e = reinterpret_cast<Engine*>(eh);                    \
-  if (!e) return fail(GS_EINVAL, "null engine");                \
+#define ENGINE(eh)                                                                           \
+  Engine* e = reinterpret_cast<Engine*>(eh);                                                 \
+  if (!e) return fail(GS_EINVAL, "null engine");                                             \
+  if (e->broken) return fail(GS_ESTATE, "engine unusable after a grid-barrier timeout; destroy it"); \
   HIPC(hipSetDevice(e->prm.device));
 
 // Zeroes every prune mask (in the multi BFS's node lines, only the mask words).
@@ -515,10 +578,15 @@ int gs_set_slots(gs_engine* eh, const gs_slot* slots, uint32_t n_slots) {
   HIPC(hipMemcpyAsync(e->obkt, ob.data(), e->S, hipMemcpyHostToDevice, e->st));
   HIPC(hipMemcpyAsync(e->min_ingress, mi.data(), e->S * 4, hipMemcpyHostToDevice, e->st));
   HIPC(hipMemcpyAsync(e->thr, thr.data(), e->S * 8, hipMemcpyHostToDevice, e->st));
-  if (e->bfs_mode == GS_BFS_MULTI) {
+  if (mv_layout(*e)) {
     std::vector<uint32_t> gtab;
     std::vector<uint2> seeds;
     mv_build_groups(*e, org, ob, bh, gtab, seeds);
+    if (e->bfs_mode == GS_BFS_HYBRID) {  // entries per node at most: the own bucket's + one per lower origin bucket
+      uint32_t parts = 1;
+      for (size_t g = 0; g < e->mv_groups.size(); ++g) parts = std::max(parts, 1 + gtab[g * GT_STRIDE + 25]);
+      if (int s_ = hb_alloc(e, parts)) return s_;
+    }
     HIPC(hipMemcpyAsync(e->mv_gtab, gtab.data(), gtab.size() * 4, hipMemcpyHostToDevice, e->st));
     HIPC(hipMemcpyAsync(e->mv_seed, seeds.data(), seeds.size() * sizeof(uint2), hipMemcpyHostToDevice, e->st));
   }
@@ -668,7 +736,7 @@ static int do_bfs(Engine* e, bool record) {
   if (int s = refuse_part(e)) return s;
   if (int s = ensure_inb(e)) return s;
   hipEvent_t t0 = nullptr;
-  const bool self_timed = e->bfs_mode == GS_BFS_MULTI;  // times its levels and its gather itself
+  const bool self_timed = mv_layout(*e);  // times its levels and its gather itself
   if (!self_timed) e->tbegin("bfs", &t0);
   hipError_t r = launch_bfs(*e, record);
   if (!self_timed) e->tend("bfs", t0);
@@ -776,7 +844,7 @@ int gs_round(gs_engine* eh, uint32_t round, int record) {
     if (int s = do_cp(e, true, true, true, rec)) return s;
   }
   if (int s = gs_chance_to_rotate(eh, round)) return s;
-  if (rec) return do_stats(e, e->bfs_mode == GS_BFS_WORKGROUP ? 2 : e->bfs_mode == GS_BFS_MULTI ? 4 : 1);
+  if (rec) return do_stats(e, e->bfs_mode == GS_BFS_WORKGROUP ? 2 : mv_layout(*e) ? 4 : 1);
   return GS_OK;
 }
 
@@ -1133,6 +1201,18 @@ int gs_engine_round_kind(gs_engine* eh, uint32_t* fused) {
   ENGINE(eh);
   if (!fused) return fail(GS_EINVAL, "null argument");
   *fused = e->fused ? 1u : 0u;
+  return GS_OK;
+}
+
+int gs_engine_bfs_geometry(gs_engine* eh, uint32_t* out, size_t n) {
+  ENGINE(eh);
+  if (!out || n < 5) return fail(GS_EINVAL, "gs_engine_bfs_geometry: need 5 words");
+  const bool on = mv_layout(*e);
+  out[0] = on ? e->mv.XT : 0;
+  out[1] = on ? e->mv.nbc : 0;
+  out[2] = on ? e->mv.nbf : 0;
+  out[3] = on ? e->mv.GW : 0;
+  out[4] = on ? (uint32_t)e->mv_groups.size() : 0;
   return GS_OK;
 }
 

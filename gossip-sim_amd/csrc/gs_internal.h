@@ -143,6 +143,15 @@ struct Engine {
   bool mv_diag = false;  // GS_MV_DIAG=1
   bool mv_line = false;   // multi: prune masks live in the row table's node lines (msu = 32)
   bool mv_fused = false;  // gs_round: gather, then k_cg_consume; GS_MV_FUSED=1: fused gather + consume (slower at C4)
+  // direction-optimizing BFS over the round's push graph (GS_BFS_HYBRID, gs_bfs_hybrid.hip);
+  // it shares the multi BFS's layout, groups, queues, T rows and record area
+  uint8_t* hb_dist = nullptr;      // [N][hb_dsp] distance of every slot of the current group
+  uint32_t hb_dsp = 16;
+  uint2* hb_pgo = nullptr;         // [N] {first, count} of each node's push-graph in-records
+  uint32_t* hb_F = nullptr;        // [3][N] slots first reached at level d (buffer d % 3)
+  unsigned long long* hb_pgr = nullptr;  // [nbc][hb_bin_cap] in-records src | slot mask << 32
+  size_t hb_bin_cap = 0;
+  uint32_t hb_parts = 0, hb_slices = 0;  // T rows per slice (entries per node at most), slices
   std::vector<uint32_t> h_nfail_any;  // host copy: slot has failed nodes
   // rotation
   uint32_t* rot_list = nullptr;
@@ -182,6 +191,7 @@ struct Engine {
 
   std::vector<gs_slot> slots;
   bool slots_set = false, failed_ranked = false;
+  bool broken = false;  // a persistent-kernel grid barrier timed out (ERR_SYNC): the engine refuses every call
 
   // profiling
   struct Timed { std::vector<std::pair<hipEvent_t, hipEvent_t>> ev; double ms = 0; uint64_t n = 0; };
@@ -254,6 +264,11 @@ void mv_build_groups(Engine& e, const std::vector<uint32_t>& origins, const std:
 // consume: gs_round's fused gather + consume (k_mv_consume) instead of the materializing
 // gather; then only k_cg_prune remains (launch_consume_prune_g(e, record, false)).
 hipError_t launch_bfs_multi(Engine& e, bool record, bool consume = false);
+// GS_BFS_HYBRID: push graph, top-down / bottom-up levels, gather (gs_bfs_hybrid.hip)
+hipError_t launch_bfs_hybrid(Engine& e, bool record);
+void hb_geometry(Engine& e, uint32_t parts);  // area / T rows / in-record regions for `parts` entries per node
+// the multi-source BFS's layout (node-major masks and egress, slot groups): MULTI and HYBRID
+inline bool mv_layout(const Engine& e) { return e.bfs_mode == GS_BFS_MULTI || e.bfs_mode == GS_BFS_HYBRID; }
 hipError_t mv_update_failures(Engine& e, const std::vector<uint32_t>& nf);
 // own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);

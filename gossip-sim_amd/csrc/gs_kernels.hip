@@ -567,6 +567,7 @@ hipError_t launch_bfs(Engine& e, bool record) {
   }
   if (e.bfs_mode == GS_BFS_BINNED) return launch_bfs_binned(e, record);
   if (e.bfs_mode == GS_BFS_MULTI) return launch_bfs_multi(e, record);
+  if (e.bfs_mode == GS_BFS_HYBRID) return launch_bfs_hybrid(e, record);
   if ((r = hipMemsetAsync(e.hops, 0xFF, e.PAIRS, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.cnt, 0, e.PAIRS * 4, e.st)) != hipSuccess) return r;
   if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st)) != hipSuccess) return r;

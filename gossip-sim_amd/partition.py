@@ -67,11 +67,13 @@ class PartitionedEngine:
         if exchange not in ("auto", "records", "dense"):
             raise ValueError("exchange must be auto, records or dense")
         self.exchange = exchange
-        # [N * S] int32 dense exchange buffer (4 * S * N bytes: 640 MB at C5's 10M x 16),
-        # allocated here -- not in the round that first goes dense, where a failed allocation
-        # on one rank would leave the others waiting in the all-reduce
+        # [N * S] int32 dense exchange buffer (4 * S * N bytes: 640 MB at C5's 10M x 16):
+        # allocated here for exchange="dense"; for "auto" only in the first round that goes
+        # dense, after every rank has agreed that its allocation succeeded (_dense_buffer), so
+        # a rank that runs out of memory fails with the others instead of leaving them waiting
+        # in the all-reduce
         self.dense = None
-        if exchange != "records":
+        if exchange == "dense":
             self.dense = torch.zeros(self.dense_words, dtype=torch.int32, device=self.dev)
         self.records = 0       # prune records of the last round (all ranks)
         self.last_mode = None  # "records" / "dense" / None (no prunes)
@@ -84,6 +86,25 @@ class PartitionedEngine:
 
     def _ptr(self, t):
         return C.c_void_p(t.data_ptr())
+
+    def _dense_buffer(self):
+        """The dense exchange buffer, allocated on first use with a MIN all-reduce of an ok
+        flag: every rank raises if any rank's allocation failed."""
+        if self.dense is not None:
+            return self.dense
+        torch = self.torch
+        buf, err = None, None
+        try:
+            buf = torch.zeros(self.dense_words, dtype=torch.int32, device=self.dev)
+        except RuntimeError as ex:  # (torch.cuda.OutOfMemoryError is a RuntimeError)
+            err = ex
+        ok = torch.tensor([0 if buf is None else 1], dtype=torch.int64, device=self.dev)
+        self.tdist.all_reduce(ok, op=self.tdist.ReduceOp.MIN, group=self.group)
+        if int(ok.item()) == 0:
+            raise RuntimeError(f"dense prune exchange: a rank could not allocate {4 * self.dense_words} bytes"
+                               + (f" (this rank: {err})" if err else ""))
+        self.dense = buf
+        return buf
 
     def _done(self):
         # the engine reads the buffers on its own stream: torch's collective must be complete
@@ -110,6 +131,7 @@ class PartitionedEngine:
                 raise RuntimeError(f"{m} prune records exceed the record buffer ({self.record_cap}); "
                                    "use exchange='auto' or 'dense'")
             if dense:
+                self._dense_buffer()
                 _check(L.gs_part_prunes_dense_out(h, self._ptr(self.dense), dev))
                 tdist.all_reduce(self.dense, group=self.group)
                 self._done()

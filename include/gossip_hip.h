@@ -54,8 +54,14 @@ enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24
  * the mask of slots reaching it at that level: one row expansion and one record
  * per pushed-to peer serve every such slot; large clusters). AUTO picks
  * WORKGROUP (n <= 8,192 and >= 64 slots), else MULTI (>= 4 slots, or >= 2 slots
- * on graphs of >= 512 coarse bins: ~4M nodes and up), else BINNED, else LEVEL. */
-enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2, GS_BFS_BINNED = 3, GS_BFS_MULTI = 4 };
+ * on graphs of >= 512 coarse bins: ~4M nodes and up), else BINNED, else LEVEL.
+ * HYBRID = direction-optimizing multi-source BFS over the round's push graph: every node's
+ * pushes for every slot built once per round as in-records grouped by destination, then
+ * levels carrying only slot masks and distances -- top-down (frontier entries, atomicOr on
+ * visited masks) for small frontiers, bottom-up (nodes still missing slots scan their
+ * in-records for pushers at the current distance) for large ones -- and one gather. */
+enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2, GS_BFS_BINNED = 3, GS_BFS_MULTI = 4,
+       GS_BFS_HYBRID = 5 };
 enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4, GS_FLAG_BINNED_ALL_LEVELS = 8,
        GS_FLAG_WIDE_RECORDS = 16, GS_FLAG_NO_SMALL_LEVELS = 32, GS_FLAG_MISPREDICT_LEVELS = 64 };
 
@@ -117,6 +123,9 @@ int gs_create(const gs_params* params, const uint64_t* stakes, uint32_t n_nodes,
               gs_engine** out);
 void gs_destroy(gs_engine* e);
 const char* gs_last_error(void);
+/* sha256 prefix (16 hex digits) of the device sources this library was built from; the
+ * profiles under profiles/ are stamped with it (not a reference interface: measurement) */
+const char* gs_kernel_hash(void);
 int gs_device_count(int* n); /* HIP devices visible to this process (0 without a GPU) */
 int gs_set_slots(gs_engine* e, const gs_slot* slots, uint32_t n_slots);
 int gs_sync(gs_engine* e); /* waits for the stream and reports deferred device-side errors */
@@ -187,6 +196,10 @@ int gs_engine_memory(gs_engine* e, uint64_t* pair_bytes, uint64_t* other_bytes);
 /* 1 if gs_round runs the one-kernel workgroup round (BFS, consume, prune and
  * statistics per slot in one workgroup), 0 if it launches the step kernels. */
 int gs_engine_round_kind(gs_engine* e, uint32_t* fused);
+/* Geometry of the multi-source / hybrid BFS (diagnostics; not a reference interface): out[0]
+ * frontier entries (multi) or nodes (hybrid) per expand slice, out[1] coarse destination bins,
+ * out[2] fine bins, out[3] slots per slot group, out[4] slot groups. n >= 5; zeros in other modes. */
+int gs_engine_bfs_geometry(gs_engine* e, uint32_t* out, size_t n);
 
 /* --- node-range partition ------------------------------
  * K engines, one per rank/GPU, created with gs_create_part on the same stakes, params

@@ -17,7 +17,7 @@ gs = eb.gs
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 U64MAX = np.uint64(2**64 - 1)
-MODES = [gs.GS_BFS_WORKGROUP, gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI]
+MODES = [gs.GS_BFS_WORKGROUP, gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI, gs.GS_BFS_HYBRID]
 
 
 def ekw(mode):
@@ -224,7 +224,7 @@ def test_round_by_round_parity_level_kernels(mode, extra):
     assert total > 0
 
 
-@pytest.mark.parametrize("mode", [gs.GS_BFS_BINNED, gs.GS_BFS_MULTI])
+@pytest.mark.parametrize("mode", [gs.GS_BFS_BINNED, gs.GS_BFS_MULTI, gs.GS_BFS_HYBRID])
 def test_parity_hub_in_degrees_above_64(mode):
     """Fanout = active-set size 32 on 500 nodes whose stakes halve every 8 stake ranks (buckets
     24 down to 0; stake ranks shuffled over the ids), inbound capacity 256: the top-stake nodes sit in most high-bucket
@@ -245,7 +245,7 @@ def test_parity_hub_in_degrees_above_64(mode):
     run_parity(n, [1, 2, 40], 22, p=0.05, mode=mode, asz=32, fanout=32, full_every=7, extra=extra, stakes=st)
 
 
-@pytest.mark.parametrize("mode", [gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI])
+@pytest.mark.parametrize("mode", [gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI, gs.GS_BFS_HYBRID])
 def test_parity_sweep_params_and_failures(mode):
     """Per-slot thresholds / min-ingress and fail-nodes (failed peers burn fanout slots)."""
     run_parity(180, [1, 3, 5, 9], 42, p=0.03, mode=mode, thr=[0.0, 0.15, 0.4, 1.0], mi=[0, 2, 3, 1],
@@ -290,7 +290,8 @@ def test_rotation_round_sequence_and_deferred_clear():
 
 @pytest.mark.parametrize("mode,narrow", [(gs.GS_BFS_LEVEL, False), (gs.GS_BFS_BINNED, False),
                                          (gs.GS_BFS_LEVEL, True), (gs.GS_BFS_BINNED, True),
-                                         (gs.GS_BFS_MULTI, False), (gs.GS_BFS_MULTI, True)])
+                                         (gs.GS_BFS_MULTI, False), (gs.GS_BFS_MULTI, True),
+                                         (gs.GS_BFS_HYBRID, False), (gs.GS_BFS_HYBRID, True)])
 def test_fused_round_matches_steps(mode, narrow):
     """gs_round's step-kernel path (consume + prune + apply of gs_consume_g.hip: register,
     wave and serial consume paths, register and wave prune paths) == the step-by-step
@@ -709,7 +710,7 @@ def test_c4_sweep_slots_1m():
     thr = [0.15] * 5 + [0.05 * (j + 1) for j in range(8)]
     S = len(fr)
     engs = [gs.Engine(st, S, seed=C2_SEED, rotation_probability=0.013333, bfs_mode=m)
-            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI)]
+            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI, gs.GS_BFS_HYBRID)]
     for e in engs:
         e.set_slots([origin] * S, 2, thr)
         e.init_active_sets()
@@ -756,7 +757,7 @@ def test_c3_widest_rows_100k():
     n = 100_000
     st = eb.synth.power_law_stakes(n)
     engs = [gs.Engine(st, 2, seed=C2_SEED, active_set_size=27, rotation_probability=0.013333, bfs_mode=m)
-            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI)]
+            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_BINNED, gs.GS_BFS_MULTI, gs.GS_BFS_HYBRID)]
     for e in engs:
         e.set_slots([int(np.argmax(st)), n // 3], 2, 0.15)
         e.init_active_sets()
@@ -791,7 +792,8 @@ def test_multi_bfs_groups_and_entries():
     equal to the level BFS in every summary, hop table, counter, cache and accumulator."""
     n, S = 3000, 70
     pks, st = eb.synth.network(n)
-    engs = [gs.Engine(st, S, seed=9, rotation_probability=0.03, bfs_mode=m) for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_MULTI)]
+    engs = [gs.Engine(st, S, seed=9, rotation_probability=0.03, bfs_mode=m)
+            for m in (gs.GS_BFS_LEVEL, gs.GS_BFS_MULTI, gs.GS_BFS_HYBRID)]
     origins = [(k * 131 + 7) % n for k in range(S - 6)] + [5, 5, 5, 77, 77, 77]  # shared origins too
     fr = [0.0, 0.1, 0.0, 0.3] * (S // 4) + [0.0] * (S % 4)
     for e in engs:
@@ -801,23 +803,25 @@ def test_multi_bfs_groups_and_entries():
     for r in range(30):
         for e in engs:
             e.round(r, record=r >= 4)
-    a, b = engs
-    np.testing.assert_array_equal(a.summaries(), b.summaries())
+    a = engs[0]
     assert int(a.summaries()["prunes"].sum()) > 0
-    for k in (0, 17, 31, 32, 50, 63, 64, 66, 69):
-        np.testing.assert_array_equal(a.hops(k), b.hops(k))
-        np.testing.assert_array_equal(a.pruned_all(k), b.pruned_all(k))
-        for x, y in zip(a.counters(k), b.counters(k)):
-            np.testing.assert_array_equal(x, y)
-        for x, y in zip(a.caches(k), b.caches(k)):
-            np.testing.assert_array_equal(x, y)
-        for x, y in zip(a.accumulators(k), b.accumulators(k)):
-            np.testing.assert_array_equal(x, y)
+    for b in engs[1:]:
+        np.testing.assert_array_equal(a.summaries(), b.summaries())
+        for k in (0, 17, 31, 32, 50, 63, 64, 66, 69):
+            np.testing.assert_array_equal(a.hops(k), b.hops(k))
+            np.testing.assert_array_equal(a.pruned_all(k), b.pruned_all(k))
+            for x, y in zip(a.counters(k), b.counters(k)):
+                np.testing.assert_array_equal(x, y)
+            for x, y in zip(a.caches(k), b.caches(k)):
+                np.testing.assert_array_equal(x, y)
+            for x, y in zip(a.accumulators(k), b.accumulators(k)):
+                np.testing.assert_array_equal(x, y)
     for e in engs:
         e.run_gossip()
-    for k in (0, 40, 69):
-        for x, y in zip(a.inbound(k), b.inbound(k)):
-            np.testing.assert_array_equal(x, y)
+    for b in engs[1:]:
+        for k in (0, 40, 69):
+            for x, y in zip(a.inbound(k), b.inbound(k)):
+                np.testing.assert_array_equal(x, y)
 
 
 def test_persistent_level_kernel_matches_default():

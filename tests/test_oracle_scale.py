@@ -89,6 +89,8 @@ VARIANTS = {  # name: engine kwargs (one origin slot each; results must be ident
     "binned_all_wide": dict(bfs_mode=gs.GS_BFS_BINNED, binned_all_levels=True, wide_records=True),
     "multi": dict(bfs_mode=gs.GS_BFS_MULTI),
     "multi_no_small": dict(bfs_mode=gs.GS_BFS_MULTI, no_small_levels=True),
+    "hybrid": dict(bfs_mode=gs.GS_BFS_HYBRID),
+    "hybrid_no_small": dict(bfs_mode=gs.GS_BFS_HYBRID, no_small_levels=True),
     "level": dict(bfs_mode=gs.GS_BFS_LEVEL),
 }
 
@@ -166,10 +168,24 @@ C4_SLOTS = [  # (origin stake rank, fail fraction, prune-stake threshold, min-in
     (2, 0.1, 0.15, 2),   # a second origin with failures
     (1, 0.5, 0.25, 2),
 ]
+# C5's shape: distinct origins (stake ranks 1..8) without failures -- every slot is a plain
+# slot whose own origin goes through the multi BFS's LDS origin hash (gs_mv_dev.h
+# mv_origin_slots) -- plus one slot with failures sharing rank 1's origin (the per-slot path
+# in the same waves)
+C5_SLOTS = [(r, 0.0, 0.15, 2) for r in range(1, 9)] + [(1, 0.1, 0.15, 2)]
+
+SWEEP_CASES = {  # id: (nodes, slots, bfs mode, environment at engine creation)
+    "c4_multi": (100_000, C4_SLOTS, gs.GS_BFS_MULTI, {}),
+    "c4_binned": (100_000, C4_SLOTS, gs.GS_BFS_BINNED, {}),
+    "c4_hybrid": (100_000, C4_SLOTS, gs.GS_BFS_HYBRID, {}),
+    # 64-node coarse bins: 625 >= 512 of them, so the multi BFS takes C5's 1,024-entry expand
+    # slices (MvGeom::XT = 1,024, chosen at >= 512 coarse bins; gs_bfs_multi.hip mv_geometry)
+    "c5_multi_wide": (40_000, C5_SLOTS, gs.GS_BFS_MULTI, {"GS_MV_BSC": "6"}),
+}
 
 
-@pytest.mark.parametrize("mode", [gs.GS_BFS_MULTI, gs.GS_BFS_BINNED])
-def test_c4_sweep_semantics_match_oracle_100k(mode):
+@pytest.mark.parametrize("case", list(SWEEP_CASES))
+def test_c4_sweep_semantics_match_oracle_100k(case, monkeypatch):
     """BASELINE C4's semantics at 100k nodes against the oracle, through the production
     round (gs_round: the BFS, k_cg_consume, k_cg_prune, the statistics kernels), with the
     sweep values as slots of ONE engine: fail fractions 0.3 / 0.1 / 0.5 at when-to-fail 0
@@ -178,16 +194,24 @@ def test_c4_sweep_semantics_match_oracle_100k(mode):
     (ReceivedCache::prune, received_cache.rs:100-131), two origins. One oracle sim per slot
     holds the engine's active sets (p = 0). For 22 rounds, through the first prune wave:
     failed sets, hops, inbound (src, hop) lists, prunes, counters, prune state, received
-    caches and the per-round summaries' integer fields."""
-    n, seed, rounds = 100_000, 0x5EED0011, 22
+    caches and the per-round summaries' integer fields. The c5 case runs C5's slot shape
+    (eight distinct origins) through the multi BFS's wide-geometry paths at 40k nodes."""
+    n, slots, mode, env = SWEEP_CASES[case]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    seed, rounds = 0x5EED0011, 22
     st = eb.synth.power_law_stakes(n)
     rank_order = np.lexsort((np.arange(n), -st.astype(np.float64)))
-    S = len(C4_SLOTS)
-    origins = [int(rank_order[r - 1]) for r, _, _, _ in C4_SLOTS]
-    fr = [f for _, f, _, _ in C4_SLOTS]
-    thr = [t for _, _, t, _ in C4_SLOTS]
-    mi = [m for _, _, _, m in C4_SLOTS]
+    S = len(slots)
+    origins = [int(rank_order[r - 1]) for r, _, _, _ in slots]
+    fr = [f for _, f, _, _ in slots]
+    thr = [t for _, _, t, _ in slots]
+    mi = [m for _, _, _, m in slots]
     eng = gs.Engine(st, S, rotation_probability=0.0, seed=seed, bfs_mode=mode)
+    for k in env:
+        monkeypatch.delenv(k)
+    if "GS_MV_BSC" in env:
+        assert eng.bfs_geometry()["expand_slice"] == 1024, eng.bfs_geometry()
     eng.set_slots(origins, mi, thr)
     eng.init_active_sets()
     peers, lens = eng.active_sets()
