@@ -14,21 +14,22 @@ waves, where pushes per origin-round settle near 3N).
 value = pushes to non-failed peers over all slots and ranks / wall time of the K
 timed steps (max over ranks).
 
-Multi-GPU (one process per GPU, no data-path collective). Default --scaling weak: the
-ranks shard a sweep of independent C2 trials -- rank r runs all 3,000 origins of the same
-stake network with Philox seed + r (its own active-set trajectory), so the per-GPU work is
-one C2 at every N (origin / parameter slices are independent units).
---scaling strong: the ranks split the 3,000 origins of ONE trial (same seed; rank r takes
-origins [r*S/K, (r+1)*S/K)), and with --check-shard rank 0 checks the gathered per-round
-summaries of every origin against all origins run on one engine. --workload c4 / c5 run
-BASELINE C4's 13 sweep sims (1M nodes) / C5's 16 origins (10M nodes) instead, dealt over
-the ranks (strong) or all on every rank as its own trial (weak). torch.distributed carries
-only the barrier, the timing max/sum and the summary gather.
+Multi-GPU (one process per GPU, no data-path collective). Default --scaling strong: the
+ranks split the 3,000 origins of ONE C2 trial (same seed; rank r takes origins
+[r*S/K, (r+1)*S/K)) -- the north star's origin-sharded sweep; with --check-shard rank 0
+checks the gathered per-round summaries of every origin against all origins run on one
+engine. At N > 1 the line also carries `weak_trial`: the ranks then run independent C2
+trials (rank r: all 3,000 origins, Philox seed + r), the per-GPU work of one C2 at every N.
+--scaling weak makes that the headline instead. --workload c4 / c5 run BASELINE C4's 13
+sweep sims (1M nodes) / C5's 16 origins (10M nodes) instead, dealt over the ranks (strong)
+or all on every rank as its own trial (weak). torch.distributed carries only the barrier,
+the timing max/sum and the summary gather.
 
 roofline: the dominant kernel (k_round_wg) with SURVEY.md 8(d) algorithmic bytes
 per launch, divided by that kernel's average duration measured with hipEvents on
 the engine stream over the timed steps; `traffic` = HBM bytes per launch from the
-committed rocprofv3 --pmc summary of the SAME round window (profiles/r02/), or null.
+committed rocprofv3 --pmc summary of the SAME round window (the newest profiles/r*/ stamped
+with the loaded library's kernel hash), or null.
 cpu_baseline: the oracle (reference-structure C++ restatement: maps keyed by
 32-byte pubkeys, one origin per sim) on all host cores (independent origin-sims
 dealt over std::threads) on a bounded sample of the same workload;
@@ -40,8 +41,8 @@ Secondary legs at N = 1 (reported beside `value`, never part of it):
       fraction of HBM peak is the north-star figure.
   c3: BASELINE C3's per-GPU share -- 100k nodes, active-set-size sweep values 12
       and 20 (sims 0 and 8 of 16 dealt over 8 GPUs), one engine per value.
-  c5: BASELINE C5's 10M-node graph on one GPU (2 origin slots, one engine): the
-      propagation work each node-range partition rank repeats.
+  c5: BASELINE C5's 10M-node graph on one GPU: origin ranks 1..16 (--c5-slots) as the
+      slots of one engine (the multi-source BFS), unpartitioned.
 """
 import argparse
 import glob
@@ -459,9 +460,9 @@ def main():
     ap.add_argument("--legs", default="c4,c3", help="with --only-large: which legs (e.g. c4 for a PMC pass)")
     ap.add_argument("--c4-sims", default="", help="c4 leg: only these of the 13 sweep sims (e.g. 0,8: a rank's share)")
     ap.add_argument("--c5-slots", type=int, default=16, help="c5 leg: origin ranks 1..K as slots (16 = C5)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: rank r runs C2 trial r (all origins, Philox seed + r); strong: the ranks split the "
-                         "origins of one trial")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="strong: the ranks split the origins of one C2 trial (default); weak: rank r runs C2 trial r "
+                         "(all origins, Philox seed + r)")
     ap.add_argument("--shard-origins", action="store_true", help="= --scaling strong")
     ap.add_argument("--per-rank-networks", action="store_true", help="= --scaling weak")
     ap.add_argument("--check-shard", action="store_true",
@@ -551,7 +552,8 @@ def main():
     assert summ.shape[0] == args.steps
     E = float(summ["pushes"].astype("float64").sum())
     V = float(summ["visited"].astype("float64").sum())
-    fused = eng.info()["fused_round"]
+    einfo = eng.info()
+    fused = einfo["fused_round"]
     k_ms, k_n = eng.kernel_time("round" if fused else "bfs")
     dt = reduce(dt_local, lambda d: d.ReduceOp.MAX)
     E_all = reduce(E, lambda d: d.ReduceOp.SUM)
@@ -593,6 +595,30 @@ def main():
             shard_check = bool(np.array_equal(full, want))
             if not shard_check:
                 raise SystemExit("origin-sharded summaries differ from the one-engine run")
+    weak_trial = None
+    if world > 1 and args.shard_origins:  # the same ranks as independent trials: rank r = all origins, seed + r
+        eng.close()
+        wt = gs.Engine(stakes, S_all, fanout=args.fanout, active_set_size=args.active_set_size,
+                       rotation_probability=args.rotation_probability, seed=args.seed + rank, device=dev,
+                       bfs_mode=args.bfs_mode, profile=False, split_round=args.split_round)
+        wt.set_slots(all_origins, args.min_ingress, args.threshold)
+        wt.init_active_sets()
+        for r in range(args.warmup):
+            wt.round(r, record=False)
+        wt.sync()
+        barrier()
+        t1 = time.perf_counter()
+        for r in range(args.warmup, args.warmup + args.steps):
+            wt.round(r, record=True)
+        wt.sync()
+        barrier()
+        dtw = reduce(time.perf_counter() - t1, lambda d: d.ReduceOp.MAX)
+        Ew = reduce(float(wt.summaries()["pushes"].astype("float64").sum()), lambda d: d.ReduceOp.SUM)
+        wt.close()
+        eng = None
+        weak_trial = {"value": Ew / dtw, "unit": "edges/s", "ms_per_step": dtw / args.steps * 1e3,
+                      "scaling": "weak", "parallelism": f"trial-sharded x{world} (rank r: all {S_all} origins, "
+                                                        f"Philox seed + r)"}
     steady = None
     if not args.no_steady and world == 1 and args.warmup + args.steps <= 60:
         for r in range(args.warmup + args.steps, 60):
@@ -633,7 +659,7 @@ def main():
                    "nodes": args.nodes, "origin_slots_per_gpu": S, "origins_total": S_all if args.shard_origins
                    else S * world, "push_fanout": args.fanout, "active_set_size": asz,
                    "rotation_probability": args.rotation_probability, "prune_stake_threshold": args.threshold,
-                   "min_ingress_nodes": args.min_ingress, "bfs_mode": eng.info()["bfs_mode"], "fused_round": fused,
+                   "min_ingress_nodes": args.min_ingress, "bfs_mode": einfo["bfs_mode"], "fused_round": fused,
                    "rounds": [args.warmup, args.warmup + args.steps],
                    "pushes_per_origin_round": E_all / (S * world * args.steps) if not args.shard_origins
                    else E_all / (S_all * args.steps),
@@ -643,10 +669,12 @@ def main():
         "roofline": roof,
         **({"steady_state": steady} if steady else {}),
         **({"shard_check": shard_check} if shard_check is not None else {}),
+        **({"weak_trial": weak_trial} if weak_trial else {}),
         **({"phases_wg_ms": phases} if phases else {}),
         "cpu_baseline": None,
     }
-    eng.close()
+    if eng is not None:
+        eng.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_all(pks, stakes, args)
         out["cpu_baseline_1core"] = cpu_baseline_1core(pks, stakes, args, args.cpu_budget)

@@ -29,6 +29,7 @@ GS_FLAG_BINNED_ALL_LEVELS = 8
 GS_FLAG_WIDE_RECORDS = 16
 GS_FLAG_NO_SMALL_LEVELS = 32
 GS_FLAG_MISPREDICT_LEVELS = 64
+GS_FLAG_FRONTIER_EXCHANGE = 128
 HOP_UNREACHED = 0xFF
 B58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
 
@@ -86,6 +87,14 @@ EXPORTS = {
     "gs_part_exchange_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
     "gs_part_prunes_dense_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_part_prunes_dense_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "gs_part_xbfs_groups": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "gs_part_xbfs_begin": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "gs_part_xbfs_expand": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    "gs_part_xbfs_send": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "gs_part_xbfs_apply": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int,
+                                     C.POINTER(C.c_uint32)]),
+    "gs_part_xbfs_end": (C.c_int, [C.c_void_p]),
+    "gs_part_xround_finish": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.POINTER(C.c_uint32)]),
     "gs_part_stats_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_part_stats_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_create": (C.c_int, [C.POINTER(Params), C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p)]),
@@ -218,7 +227,7 @@ class Engine:
     def __init__(self, stakes, n_slots, *, fanout=6, active_set_size=12, rotation_probability=0.013333, seed=0,
                  device=0, bfs_mode=GS_BFS_AUTO, inbound_capacity=0, profile=False, split_round=False,
                  narrow_wave_path=False, binned_all_levels=False, wide_records=False, no_small_levels=False,
-                 mispredict_levels=False, part=None):
+                 mispredict_levels=False, frontier_exchange=False, part=None):
         L = lib()
         self.stakes = np.ascontiguousarray(stakes, dtype=np.uint64)
         self.n = len(self.stakes)
@@ -229,7 +238,8 @@ class Engine:
                    (GS_FLAG_NARROW_WAVE_PATH if narrow_wave_path else 0) |
                    (GS_FLAG_BINNED_ALL_LEVELS if binned_all_levels else 0) |
                    (GS_FLAG_WIDE_RECORDS if wide_records else 0) | (GS_FLAG_NO_SMALL_LEVELS if no_small_levels else 0) |
-                   (GS_FLAG_MISPREDICT_LEVELS if mispredict_levels else 0))
+                   (GS_FLAG_MISPREDICT_LEVELS if mispredict_levels else 0) |
+                   (GS_FLAG_FRONTIER_EXCHANGE if frontier_exchange else 0))
         h = C.c_void_p()
         if part is None:
             _check(L.gs_create(C.byref(p), _ptr(self.stakes), self.n, n_slots, C.byref(h)))

@@ -142,11 +142,11 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
     a.ctr[0] = 0;  // expand(d) is done with it; expand(d + 1) starts at 0
     if (pi != MV_NOPAIR) a.dpair[pi + 1] = qn ? d + 1 : d;
   }
-  if (qn == 0) return;
+  if (qn == 0 && !a.xrows) return;  // (an exchange partition applies what other ranks pushed to it)
   const uint32_t c = mv_xcd_bin(blockIdx.x, a.nbc);
   if (c >= a.nbc) return;
   const uint32_t tid = threadIdx.x, BSC = a.BSC, UB = a.UB, BP = 1u << BSC, BPm = BP - 1;
-  const uint32_t G = (qn + a.XT - 1) / a.XT;
+  const uint32_t G = a.xrows ? a.xrows : (qn + a.XT - 1) / a.XT;
   const uint32_t v0 = c << BSC, nv = min(BP, a.N - v0);
   // GS_PHASE_PROFILE: thread 0's clocks at pclk[16..19] (T column + scan, vis load, records, tail)
   unsigned long long tm = a.pclk && tid == 0 ? wall_clock64() : 0;
@@ -1059,6 +1059,95 @@ __global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void
   if (errf) atomicOr(a.err, errf);
 }
 
+// ------------------------------------------ frontier exchange (node-range partition) ----
+// A frontier-exchange partition rank (GS_FLAG_FRONTIER_EXCHANGE) expands only the frontier
+// entries of the nodes it owns; level d's push records (the expand runs, binned by coarse
+// destination bin) go to the rank owning each bin, which applies them (k_mv_apply: first
+// arrivals in its LDS copy of the bin's visited masks, pool records, its own next-level
+// entries). Ranks own whole coarse bins, so a bin's records go to one rank.
+
+// Records per coarse bin in level d's G expand runs (the T column of bin c).
+__global__ __launch_bounds__(256) void k_mvx_bincount(MvArgs a, uint32_t G, uint32_t* __restrict__ bincnt) {
+  __shared__ uint32_t part[4];
+  const uint32_t c = blockIdx.x;
+  uint32_t s = 0;
+  for (uint32_t i = threadIdx.x; i < G; i += 256) {
+    const uint32_t* Tr = a.T + (size_t)i * a.TW;
+    s += Tr[2 + c] - Tr[1 + c];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) bincnt[c] = part[0] + part[1] + part[2] + part[3];
+}
+
+// Bin c's segments of the G expand runs, copied contiguously (slice order) to out[rpos[c]..],
+// and its record count to out[hpos[c]]: the header word of the owner's message.
+__global__ __launch_bounds__(256) void k_mvx_pack(MvArgs a, uint32_t G, const unsigned long long* __restrict__ hpos,
+                                                  const unsigned long long* __restrict__ rpos,
+                                                  const uint32_t* __restrict__ bincnt,
+                                                  unsigned long long* __restrict__ out) {
+  __shared__ uint32_t pre[MV_SEG + 1], sb[MV_SEG], wsum[16];
+  const uint32_t c = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) out[hpos[c]] = bincnt[c];
+  size_t dst = rpos[c];
+  for (uint32_t c0 = 0; c0 < G; c0 += MV_SEG) {
+    const uint32_t gc = min(MV_SEG, G - c0);
+    for (uint32_t i = tid; i < gc; i += 256) {
+      const uint32_t* Tr = a.T + (size_t)(c0 + i) * a.TW;
+      const uint32_t st = Tr[1 + c];
+      pre[i] = Tr[2 + c] - st;
+      sb[i] = Tr[0] + st;
+    }
+    __syncthreads();
+    const uint32_t ct = mv_block_scan(pre, gc, wsum);
+    if (tid == 0) pre[gc] = ct;
+    __syncthreads();
+    for (uint32_t r = tid; r < ct; r += 256) {
+      uint32_t lo = 0, hi = gc;  // largest i with pre[i] <= r
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= r) lo = mid; else hi = mid;
+      }
+      out[dst + r] = a.area[sb[lo] + (r - pre[lo])];
+    }
+    dst += ct;
+    __syncthreads();
+  }
+}
+
+// T row q of a received level: sender q's message (words off[q] ..) is nbm header words
+// (record counts of this rank's bins blo, blo + 1, ...) then the records, bin by bin.
+__global__ __launch_bounds__(64) void k_mvx_trows(const unsigned long long* __restrict__ recv,
+                                                  const unsigned long long* __restrict__ off, uint32_t blo, uint32_t nbm,
+                                                  uint32_t nbc, uint32_t TW, uint32_t* __restrict__ T) {
+  const uint32_t q = blockIdx.x;
+  uint32_t* Tr = T + (size_t)q * TW;
+  const unsigned long long o = off[q];
+  for (uint32_t b = threadIdx.x; b < blo; b += 64) Tr[1 + b] = 0;
+  if (threadIdx.x == 0) {
+    Tr[0] = (uint32_t)(o + nbm);
+    uint32_t run = 0;
+    for (uint32_t i = 0; i < nbm; ++i) {
+      Tr[1 + blo + i] = run;
+      run += (uint32_t)recv[o + i];
+    }
+    for (uint32_t b = blo + nbm; b <= nbc; ++b) Tr[1 + b] = run;
+  }
+}
+
+// The group's origins owned by this rank: visited masks and level-0 entries (lvl was zeroed).
+__global__ void k_mvx_seed(MvArgs a, const uint2* __restrict__ seeds, uint32_t nseed, uint2* __restrict__ q0) {
+  const uint32_t i = threadIdx.x;
+  if (i >= nseed) return;
+  const uint2 sd = seeds[i];
+  const uint32_t o = sd.x & 0xFFFFFFu;
+  if (o - a.vlo >= a.vhi - a.vlo) return;
+  a.vis[o] = sd.y;
+  q0[atomicAdd(&a.lvl[0], 1u)] = sd;
+}
+
 // fcls[w] = smallest i (1-based) with frank[w] < T[i-1] over the ascending distinct
 // failure counts T[0..m); 255 when w fails in no slot.
 __global__ void k_mv_fcls(const uint32_t* __restrict__ frank, const uint32_t* __restrict__ T, uint32_t m, uint32_t N,
@@ -1210,6 +1299,7 @@ MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
   a.vlo = e.vlo; a.vhi = e.vlo + e.NP; a.NP = e.NP; a.MSU = (uint32_t)e.msu;
   a.XT = e.mv.XT;
+  a.xrows = 0;
   a.small = e.mv_pgrid ? MV_PSMALL : MV_SMALL;  // the persistent kernel's bound, or the one-workgroup kernel's
   if (const char* sm = std::getenv("GS_MV_SMALL")) a.small = (uint32_t)std::strtoul(sm, nullptr, 10);
   if (e.prm.flags & GS_FLAG_NO_SMALL_LEVELS) a.small = 0;  // every level through expand + apply
@@ -1347,7 +1437,8 @@ static hipError_t mv_group_polled(Engine& e, MvArgs& a, const MvGroup& gr, uint3
   }
 }
 
-hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
+// Dynamic-LDS limits of the level kernels (once per engine) and the persistent kernel's grid.
+static hipError_t mv_attrs(Engine& e) {
   hipError_t r = hipSuccess;
   const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)e.mv.XT * e.ASZP * 8;
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
@@ -1393,6 +1484,17 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     }
     e.mv_attr_set = true;
   }
+  return r;
+}
+
+hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
+  hipError_t r = hipSuccess;
+  const size_t lds_x = mv_hist_bytes(e.mv.nbc) + (size_t)e.mv.XT * e.ASZP * 8;
+  const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
+  const size_t lds_g = mv_glds();
+  const uint32_t fno = mv_kept_bins(e);
+  const size_t lds_s = fno <= MV_SMALL_LP ? (size_t)fno * 4 : 0;
+  if ((r = mv_attrs(e))) return r;
   const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8;
   const uint32_t ggrid = fno;
   const uint32_t xgrid = 2048;
@@ -1478,6 +1580,110 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       std::fprintf(stderr, "\n");
     }
   }
+  return hipGetLastError();
+}
+
+// ------------------------------------------ frontier exchange: host side ----
+// The owner of coarse bin c, and rank q's first bin and bin count (ranks own whole bins).
+static uint32_t mvx_owner(const Engine& e, uint32_t c) {
+  return (uint32_t)(((size_t)c << e.mv.BSC) / e.part_C);
+}
+static void mvx_bins(const Engine& e, uint32_t q, uint32_t& first, uint32_t& nb) {
+  const size_t lo = std::min<size_t>(e.N, (size_t)q * e.part_C), hi = std::min<size_t>(e.N, lo + e.part_C);
+  first = (uint32_t)(lo >> e.mv.BSC);
+  nb = (uint32_t)(((hi + (1u << e.mv.BSC) - 1) >> e.mv.BSC) - first);
+  if (hi <= lo) nb = 0;
+}
+
+hipError_t mvx_begin(Engine& e, uint32_t g, uint32_t& n_local) {
+  hipError_t r;
+  if ((r = mv_attrs(e))) return r;
+  const MvGroup& gr = e.mv_groups[g];
+  MvArgs a = mv_args(e, gr, g);
+  if ((r = hipMemsetAsync(e.mv_vis, 0, (size_t)e.N * 4, e.st))) return r;
+  if ((r = hipMemsetAsync(e.lvl, 0, 256 * 4, e.st))) return r;
+  if ((r = hipMemsetAsync(e.mv_pused, 0, (size_t)mv_kept_bins(e) * 4, e.st))) return r;
+  if (gr.nseed > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_mvx_seed, dim3(1), dim3(1024), 0, e.st, a, e.mv_seed + gr.seed0, gr.nseed, e.mv_q[0]);
+  if ((r = hipMemcpyAsync(e.h_err + 1, e.lvl, 4, hipMemcpyDeviceToHost, e.st))) return r;
+  if ((r = hipStreamSynchronize(e.st))) return r;
+  n_local = e.h_err[1];
+  return hipGetLastError();
+}
+
+hipError_t mvx_expand(Engine& e, uint32_t g, uint32_t d, uint32_t n_local, std::vector<uint64_t>& words_to) {
+  hipError_t r;
+  MvArgs a = mv_args(e, e.mv_groups[g], g);
+  const uint32_t nbc = e.mv.nbc, K = e.part_K;
+  const uint32_t G = (n_local + e.mv.XT - 1) / e.mv.XT;
+  if ((size_t)n_local > e.mv.q_cap || G > e.mv.rows_cap) return hipErrorInvalidValue;
+  std::vector<uint32_t> cnt(nbc, 0);
+  if (G) {
+    const size_t lds_x = mv_hist_bytes(nbc) + (size_t)e.mv.XT * e.ASZP * 8;
+    launch_expand(e, a, d, MV_NOPAIR, lds_x, std::min<uint32_t>(G, 2048));
+    hipLaunchKernelGGL(k_mvx_bincount, dim3(nbc), dim3(256), 0, e.st, a, G, e.x_bincnt);
+    if ((r = hipMemcpyAsync(cnt.data(), e.x_bincnt, nbc * 4, hipMemcpyDeviceToHost, e.st))) return r;
+    if ((r = hipStreamSynchronize(e.st))) return r;
+  } else {
+    if ((r = hipMemsetAsync(e.x_bincnt, 0, nbc * 4, e.st))) return r;
+  }
+  // message to rank q: the counts of q's bins (one u64 word each), then their records in bin order
+  std::vector<unsigned long long> pos(2 * (size_t)nbc);
+  words_to.assign(K, 0);
+  std::vector<uint64_t> start(K + 1, 0);
+  for (uint32_t q = 0; q < K; ++q) {
+    uint32_t f, nb;
+    mvx_bins(e, q, f, nb);
+    uint64_t w = nb;
+    for (uint32_t i = 0; i < nb; ++i) w += cnt[f + i];
+    words_to[q] = w;
+    start[q + 1] = start[q] + w;
+  }
+  if (start[K] > e.x_send_cap) return hipErrorInvalidValue;
+  for (uint32_t q = 0; q < K; ++q) {
+    uint32_t f, nb;
+    mvx_bins(e, q, f, nb);
+    uint64_t rp = start[q] + nb;
+    for (uint32_t i = 0; i < nb; ++i) {
+      pos[f + i] = start[q] + i;       // header word
+      pos[nbc + f + i] = rp;           // records
+      rp += cnt[f + i];
+    }
+  }
+  if ((r = hipMemcpyAsync(e.x_pos, pos.data(), pos.size() * 8, hipMemcpyHostToDevice, e.st))) return r;
+  hipLaunchKernelGGL(k_mvx_pack, dim3(nbc), dim3(256), 0, e.st, a, G, e.x_pos, e.x_pos + nbc, e.x_bincnt, e.x_send);
+  e.x_send_words = start[K];
+  if ((r = hipStreamSynchronize(e.st))) return r;  // (pos is a host temporary)
+  return hipGetLastError();
+}
+
+hipError_t mvx_apply(Engine& e, uint32_t g, uint32_t d, const unsigned long long* recv,
+                     const std::vector<uint64_t>& words_from, uint32_t& n_next) {
+  hipError_t r;
+  MvArgs a = mv_args(e, e.mv_groups[g], g);
+  const uint32_t K = e.part_K;
+  std::vector<unsigned long long> off(K + 1, 0);
+  for (uint32_t q = 0; q < K; ++q) off[q + 1] = off[q] + words_from[q];
+  if (off[K] > 0xFFFFFFF0ull) return hipErrorInvalidValue;  // (T rows hold u32 record places)
+  uint32_t blo, nbm;
+  mvx_bins(e, e.part_rank, blo, nbm);
+  if ((r = hipMemcpyAsync(e.x_off, off.data(), (K + 1) * 8, hipMemcpyHostToDevice, e.st))) return r;
+  hipLaunchKernelGGL(k_mvx_trows, dim3(K), dim3(64), 0, e.st, recv, e.x_off, blo, nbm, e.mv.nbc, e.mv.TW, e.x_T);
+  a.T = e.x_T;
+  a.area = const_cast<unsigned long long*>(recv);
+  a.xrows = K;
+  const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
+  const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8;
+  hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, d, MV_NOPAIR, e.mv_q[0], e.mv_q[1]);
+  if ((r = hipMemcpyAsync(e.h_err + 1, e.lvl + d + 1, 4, hipMemcpyDeviceToHost, e.st))) return r;
+  if ((r = hipStreamSynchronize(e.st))) return r;
+  n_next = e.h_err[1];
+  return hipGetLastError();
+}
+
+hipError_t mvx_gather(Engine& e, uint32_t g) {
+  MvArgs a = mv_args(e, e.mv_groups[g], g);
+  hipLaunchKernelGGL(k_mv_gather, dim3(mv_kept_bins(e)), dim3(MV_GT), mv_glds(), e.st, a);
   return hipGetLastError();
 }
 

@@ -115,6 +115,8 @@ static void destroy_engine(Engine* e) {
   for (void* p : e->allocs) hipFree(p);
   if (e->h_err) hipHostFree(e->h_err);
   if (e->part_in) hipFree(e->part_in);
+  if (e->x_recv) hipFree(e->x_recv);
+  if (e->x_pin) hipHostFree(e->x_pin);
   if (e->mv_hlvl) hipHostFree(e->mv_hlvl);
   if (e->mv_prof) hipHostFree(e->mv_prof);
   for (auto& kv : e->timers)
@@ -266,13 +268,18 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
       return fail(GS_EINVAL, "a node-range partition runs bfs_mode GS_BFS_MULTI (or AUTO)");
     }
     mode = GS_BFS_MULTI;
-    const uint32_t C = (((n + K - 1) / K) + 1023) & ~1023u;  // whole 1,024-node bins per rank
+    // whole 1,024-node bins per rank; a frontier-exchange rank owns whole coarse bins too (its
+    // level records go to one owner per bin)
+    e->part_x = (prm->flags & GS_FLAG_FRONTIER_EXCHANGE) != 0;
+    const uint32_t unit = e->part_x ? std::max<uint32_t>(1024, 1u << e->mv.BSC) : 1024u;
+    const uint32_t C = (uint32_t)((((size_t)n + K - 1) / K + unit - 1) / unit * unit);
     const uint32_t lo = (uint32_t)std::min<uint64_t>(n, (uint64_t)rank * C), hi = std::min(n, lo + C);
     if (lo >= hi) {
       destroy_engine(e);
       return fail(GS_EINVAL, "node-range partition: rank owns no nodes (ranges are multiples of 1,024 ids)");
     }
     e->part_on = true;
+    e->part_C = C;
     e->part_K = K;
     e->part_rank = rank;
     e->part_lo = lo;
@@ -312,6 +319,12 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     return fail(GS_EINVAL, "bfs_mode");
   }
   e->bfs_mode = mode;
+  if (e->part_x) {  // a frontier-exchange rank's queues and level area hold its own nodes' entries only
+    MvGeom& g = e->mv;
+    g.q_cap = (size_t)e->NP * std::min<size_t>(std::min<size_t>(n_slots, g.GW), 26) + 64;
+    g.rows_cap = (g.q_cap + g.XT - 1) / g.XT + 1;
+    g.area_cap = g.rows_cap * g.XT * e->ASZ;
+  }
   const bool mvl = mv_layout(*e);
   e->inb_valid = !mvl;  // multi / hybrid: no inbound rows until a BFS writes them
   if (mode == GS_BFS_HYBRID) {  // no pool records: slot groups limited by the level records only
@@ -468,6 +481,14 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     e->pair_bytes += e->dev_bytes - b1;
     ALLOC(e->part_cnt, 1, 0);
     ALLOC(e->part_stats, part_stats_words(*e), 0);
+    if (e->part_x) {
+      e->x_send_cap = e->mv.area_cap + e->mv.nbc;
+      ALLOC(e->x_send, e->x_send_cap, 0);
+      ALLOC(e->x_T, (size_t)K * e->mv.TW, 0);
+      ALLOC(e->x_bincnt, e->mv.nbc, 0);
+      ALLOC(e->x_pos, 2 * (size_t)e->mv.nbc, 0);
+      ALLOC(e->x_off, (size_t)K + 1, 0);
+    }
   }
   if (const char* pp = std::getenv("GS_PHASE_PROFILE"); pp && pp[0] == '1') ALLOC(e->phase_clk, 32, 0);
 
@@ -1319,6 +1340,7 @@ int gs_part_sizes(gs_engine* eh, size_t* stats_words, uint32_t* lo, uint32_t* hi
 
 int gs_part_round(gs_engine* eh, uint32_t round, int record, uint32_t* n_records) {
   PART(eh);
+  if (e->part_x) return fail(GS_ESTATE, "a frontier-exchange rank runs its BFS with gs_part_xbfs_* (and gs_part_xround_finish)");
   if (!n_records) return fail(GS_EINVAL, "null argument");
   if (int s = need_slots(e)) return s;
   if (round >= (1u << 27)) return fail(GS_ERANGE, "round index must be < 2^27");
@@ -1339,6 +1361,119 @@ int gs_part_round(gs_engine* eh, uint32_t round, int record, uint32_t* n_records
   HIPC(hipStreamSynchronize(e->st));
   if (int s = check_err(e)) return s;
   e->part_nrec = e->h_err[1];  // (more than part_rec_cap: only the dense exchange can carry this round)
+  *n_records = e->part_nrec;
+  return GS_OK;
+}
+
+#define PARTX(eh)                                                                               \
+  PART(eh);                                                                                     \
+  if (!e->part_x) return fail(GS_ESTATE, "not a frontier-exchange rank (GS_FLAG_FRONTIER_EXCHANGE)");
+
+int gs_part_xbfs_groups(gs_engine* eh, uint32_t* n_groups) {
+  PARTX(eh);
+  if (int s = need_slots(e)) return s;
+  if (!n_groups) return fail(GS_EINVAL, "null argument");
+  *n_groups = (uint32_t)e->mv_groups.size();
+  return GS_OK;
+}
+
+int gs_part_xbfs_begin(gs_engine* eh, uint32_t group, uint32_t* n_local) {
+  PARTX(eh);
+  if (int s = need_slots(e)) return s;
+  if (!n_local || group >= e->mv_groups.size()) return fail(GS_EINVAL, "bad group / null argument");
+  if (int s = flush_rot_clear(e)) return s;
+  if (int s = ensure_inb(e)) return s;
+  if (group == 0) HIPC(hipMemsetAsync(e->part_cnt, 0, 4, e->st));
+  e->x_group = group;
+  e->x_level = 0;
+  e->tbegin("bfs", &e->x_t0);
+  HIPC(mvx_begin(*e, group, e->x_nlocal));
+  *n_local = e->x_nlocal;
+  return GS_OK;
+}
+
+int gs_part_xbfs_expand(gs_engine* eh, uint32_t level, uint64_t* words_to) {
+  PARTX(eh);
+  if (e->x_group == 0xFFFFFFFFu || level != e->x_level || !words_to)
+    return fail(GS_ESTATE, "gs_part_xbfs_expand: begin the group first and take the levels in order");
+  if (level >= 254) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
+  std::vector<uint64_t> w;
+  HIPC(mvx_expand(*e, e->x_group, level, e->x_nlocal, w));
+  for (uint32_t q = 0; q < e->part_K; ++q) words_to[q] = w[q];
+  return check_err(e);
+}
+
+int gs_part_xbfs_send(gs_engine* eh, void* dst, int dev) {
+  PARTX(eh);
+  if (!dst) return fail(GS_EINVAL, "null argument");
+  if (e->x_send_words) HIPC(hipMemcpyAsync(dst, e->x_send, e->x_send_words * 8, kind_to(dev), e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  return GS_OK;
+}
+
+int gs_part_xbfs_apply(gs_engine* eh, uint32_t level, const void* src, const uint64_t* words_from, int dev,
+                       uint32_t* n_local) {
+  PARTX(eh);
+  if (e->x_group == 0xFFFFFFFFu || level != e->x_level || !words_from || !n_local)
+    return fail(GS_ESTATE, "gs_part_xbfs_apply: after gs_part_xbfs_expand of the same level");
+  std::vector<uint64_t> wf(words_from, words_from + e->part_K);
+  size_t total = 0;
+  for (uint64_t x : wf) total += x;
+  const unsigned long long* rec = reinterpret_cast<const unsigned long long*>(src);
+  if (!dev && total) {  // host messages: through a pinned host buffer into a grow-only device buffer
+    if (total > e->x_recv_cap) {
+      HIPC(hipStreamSynchronize(e->st));
+      if (e->x_recv) hipFree(e->x_recv);
+      if (e->x_pin) hipHostFree(e->x_pin);
+      e->x_recv = nullptr;
+      e->x_pin = nullptr;
+      e->x_recv_cap = 0;
+      HIPC(hipMalloc(&e->x_recv, total * 8));
+      HIPC(hipHostMalloc(&e->x_pin, total * 8, hipHostMallocDefault));
+      e->x_recv_cap = total;
+
+    }
+    HIPC(hipStreamSynchronize(e->st));  // (the previous level's copy out of x_pin is done)
+    std::memcpy(e->x_pin, src, total * 8);
+    HIPC(hipMemcpyAsync(e->x_recv, e->x_pin, total * 8, hipMemcpyHostToDevice, e->st));
+    rec = e->x_recv;
+  }
+  if (!rec) return fail(GS_EINVAL, "null messages");
+  HIPC(mvx_apply(*e, e->x_group, level, rec, wf, e->x_nlocal));
+  e->x_level = level + 1;
+  *n_local = e->x_nlocal;
+  return check_err(e);
+}
+
+int gs_part_xbfs_end(gs_engine* eh) {
+  PARTX(eh);
+  if (e->x_group == 0xFFFFFFFFu) return fail(GS_ESTATE, "gs_part_xbfs_end: no group begun");
+  e->tend("bfs", e->x_t0);
+  hipEvent_t t0;
+  e->tbegin("gather", &t0);
+  HIPC(mvx_gather(*e, e->x_group));
+  e->tend("gather", t0);
+  e->x_group = 0xFFFFFFFFu;
+  e->inb_valid = true;
+  return check_err(e);
+}
+
+int gs_part_xround_finish(gs_engine* eh, uint32_t round, int record, uint32_t* n_records) {
+  PARTX(eh);
+  if (!n_records) return fail(GS_EINVAL, "null argument");
+  if (round >= (1u << 27)) return fail(GS_ERANGE, "round index must be < 2^27");
+  const bool rec = record != 0;
+  hipEvent_t t0;
+  e->tbegin("consume", &t0);
+  hipError_t r = hipMemsetAsync(e->slot_prunes, 0, e->S * 4, e->st);
+  if (r == hipSuccess) r = launch_consume_prune_g(*e, rec, true);  // consume + send_prunes of own nodes
+  if (r == hipSuccess) r = launch_part_emit(*e);                   // ... as records for the other ranks
+  e->tend("consume", t0);
+  HIPC(r);
+  HIPC(hipMemcpyAsync(e->h_err + 1, e->part_cnt, 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  if (int s = check_err(e)) return s;
+  e->part_nrec = e->h_err[1];
   *n_records = e->part_nrec;
   return GS_OK;
 }

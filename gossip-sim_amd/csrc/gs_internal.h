@@ -174,6 +174,22 @@ struct Engine {
   uint2* part_in = nullptr;         // every rank's prune records (gs_part_prunes_in), grow-only
   size_t part_in_cap = 0;
   uint64_t* part_stats = nullptr;   // packed stats partials [S][5 + 256 + bm_words]
+  // frontier-exchange partition (GS_FLAG_FRONTIER_EXCHANGE): this rank expands its own frontier
+  // and exchanges each level's push records with the owners of their destination bins
+  bool part_x = false;
+  uint32_t part_C = 0;                  // nodes per rank (whole coarse bins)
+  unsigned long long* x_send = nullptr;  // packed messages of the level [x_send_cap] u64
+  size_t x_send_cap = 0, x_send_words = 0;
+  unsigned long long* x_recv = nullptr;  // host-exchanged messages staged on the device (grow-only)
+  unsigned long long* x_pin = nullptr;   // pinned host staging of host-exchanged messages
+  size_t x_recv_cap = 0;
+  uint32_t* x_T = nullptr;              // [K][TW] T rows of the received level
+  uint32_t* x_bincnt = nullptr;         // [nbc]
+  unsigned long long* x_pos = nullptr;  // [2][nbc] header / record places in x_send
+  unsigned long long* x_off = nullptr;  // [K + 1]
+  uint32_t x_group = 0xFFFFFFFFu, x_level = 0;
+  uint32_t x_nlocal = 0;
+  hipEvent_t x_t0 = nullptr;           // (timing of the group's levels)
   // stats
   uint32_t* rs_u32 = nullptr;   // per slot: visited, pushes, stranded, pad
   uint64_t* rs_ssum = nullptr;  // per slot: stranded stake sum
@@ -270,6 +286,12 @@ void hb_geometry(Engine& e, uint32_t parts);  // area / T rows / in-record regio
 // the multi-source BFS's layout (node-major masks and egress, slot groups): MULTI and HYBRID
 inline bool mv_layout(const Engine& e) { return e.bfs_mode == GS_BFS_MULTI || e.bfs_mode == GS_BFS_HYBRID; }
 hipError_t mv_update_failures(Engine& e, const std::vector<uint32_t>& nf);
+// frontier-exchange partition levels (gs_bfs_multi.hip): seed, expand + pack, apply, gather
+hipError_t mvx_begin(Engine& e, uint32_t g, uint32_t& n_local);
+hipError_t mvx_expand(Engine& e, uint32_t g, uint32_t d, uint32_t n_local, std::vector<uint64_t>& words_to);
+hipError_t mvx_apply(Engine& e, uint32_t g, uint32_t d, const unsigned long long* recv,
+                     const std::vector<uint64_t>& words_from, uint32_t& n_next);
+hipError_t mvx_gather(Engine& e, uint32_t g);
 // own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);

@@ -58,6 +58,7 @@ struct MvArgs {
   uint32_t MSU;  // node stride of the masks (SP, or 32 in node lines)
   uint32_t XT;   // frontier entries per expand slice (MV_XT or MV_XT_L; mv_geometry)
   uint32_t small;  // levels of at most this many entries run in the one-workgroup kernel
+  uint32_t xrows;  // frontier-exchange partition: apply walks this many T rows (one per sender rank), else 0
   size_t PAIRS, area_cap, rows_cap, q_cap, pcap;
   // direction-optimizing BFS over the round's push graph (gs_bfs_hybrid.hip)
   uint8_t* dist;              // [N][DSP] each slot's BFS distance (0xFF: not reached)

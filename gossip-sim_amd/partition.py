@@ -29,33 +29,54 @@ import numpy as np
 from . import GS_BFS_MULTI, Engine, _check, lib
 
 
-def partition_ranges(n, world):
-    """The node ranges gs_create_part gives ranks 0..world-1: contiguous, whole 1,024-id
-    bins of ceil(n / world) rounded up. Raises ValueError when a trailing rank would own
-    no node (e.g. n = 3,000 over 4 ranks) -- identically on every rank, before any engine
-    or collective exists, so no rank is left waiting in a collective."""
-    c = ((-(-n // world)) + 1023) & ~1023
+def coarse_bin_nodes(n):
+    """Nodes per coarse destination bin of the multi-source BFS for an n-node graph (the
+    rule of gs_bfs_multi.hip mv_geometry: about 256 bins, 2^6 .. 2^13 nodes each)."""
+    ub = max(1, (n - 1).bit_length())
+    return 1 << min(13, max(6, ub - 8 if ub > 8 else 0))
+
+
+def partition_unit(n, frontier=False):
+    """Node ids per partition unit: 1,024; a frontier-exchange partition owns whole coarse
+    bins as well (each level's records for a bin go to one rank)."""
+    return max(1024, coarse_bin_nodes(n)) if frontier else 1024
+
+
+def partition_ranges(n, world, frontier=False):
+    """The node ranges gs_create_part gives ranks 0..world-1: contiguous, whole units
+    (partition_unit) of ceil(n / world) rounded up. Raises ValueError when a trailing rank
+    would own no node (e.g. n = 3,000 over 4 ranks) -- identically on every rank, before any
+    engine or collective exists, so no rank is left waiting in a collective."""
+    unit = partition_unit(n, frontier)
+    c = -(-(-(-n // world)) // unit) * unit
     out = [(min(n, r * c), min(n, r * c + c)) for r in range(world)]
     if any(lo >= hi for lo, hi in out):
         raise ValueError(f"a node-range partition of {n} nodes over {world} ranks leaves a rank without nodes "
-                         f"(ranges are whole 1,024-id bins of {c}); use at most {-(-n // c)} ranks")
+                         f"(ranges are whole {unit}-id units of {c}); use at most {-(-n // c)} ranks")
     return out
 
 
 class PartitionedEngine:
-    def __init__(self, stakes, n_slots, *, group=None, device=0, exchange="auto", **engine_kw):
+    def __init__(self, stakes, n_slots, *, group=None, device=0, exchange="auto", bfs="replicated", **engine_kw):
         import torch
         import torch.distributed as tdist
         self.torch, self.tdist, self.group = torch, tdist, group
         self.rank = tdist.get_rank(group)
         self.world = tdist.get_world_size(group)
         engine_kw["bfs_mode"] = GS_BFS_MULTI
-        partition_ranges(len(stakes), self.world)  # (raises the same on every rank)
-        self.eng = Engine(stakes, n_slots, device=device, part=(self.rank, self.world), **engine_kw)
+        if bfs not in ("replicated", "frontier"):
+            raise ValueError("bfs must be replicated or frontier")
+        self.frontier = bfs == "frontier"
+        ranges = partition_ranges(len(stakes), self.world, self.frontier)  # (raises the same on every rank)
+        self.eng = Engine(stakes, n_slots, device=device, part=(self.rank, self.world),
+                          frontier_exchange=self.frontier, **engine_kw)
         sw = C.c_size_t()
         lo, hi = C.c_uint32(), C.c_uint32()
         _check(lib().gs_part_sizes(self.eng.h, C.byref(sw), C.byref(lo), C.byref(hi)))
         self.node_lo, self.node_hi = lo.value, hi.value
+        assert (self.node_lo, self.node_hi) == ranges[self.rank], (self.node_lo, self.node_hi, ranges)
+        self.levels = 0         # BFS levels of the last round (frontier exchange)
+        self.level_bytes = 0    # frontier-exchange bytes this rank received over all rounds
         self.on_device = tdist.get_backend(group) == "nccl"
         if self.on_device:
             torch.cuda.set_device(device)
@@ -111,11 +132,55 @@ class PartitionedEngine:
         if self.on_device:
             self.torch.cuda.synchronize()
 
+    def _frontier_bfs(self):
+        """Cluster::run_gossip (gossip.rs:494-615) over the partition with a frontier exchange
+        per level: each rank expands only its own frontier entries; the level's push records
+        go to the ranks owning their destinations (two all-to-alls: the counts, then the
+        messages), which apply them; the BFS ends when no rank has a next-level entry."""
+        torch, tdist, L, h, dev = self.torch, self.tdist, lib(), self.eng.h, int(self.on_device)
+        K = self.world
+        ng = C.c_uint32()
+        _check(L.gs_part_xbfs_groups(h, C.byref(ng)))
+        n = C.c_uint32()
+        wto = np.zeros(K, dtype=np.uint64)
+        wfrom = np.zeros(K, dtype=np.uint64)
+        levels = 0
+        for g in range(ng.value):
+            _check(L.gs_part_xbfs_begin(h, g, C.byref(n)))
+            tot = torch.tensor([n.value], dtype=torch.int64, device=self.dev)
+            tdist.all_reduce(tot, group=self.group)
+            d = 0
+            while int(tot.item()) > 0:
+                _check(L.gs_part_xbfs_expand(h, d, wto.ctypes.data_as(C.c_void_p)))
+                cto = torch.tensor(wto.astype(np.int64), device=self.dev)
+                cfrom = torch.zeros(K, dtype=torch.int64, device=self.dev)
+                tdist.all_to_all_single(cfrom, cto, group=self.group)
+                wfrom[:] = cfrom.cpu().numpy().astype(np.uint64)
+                send = torch.empty(int(wto.sum()), dtype=torch.int64, device=self.dev)
+                _check(L.gs_part_xbfs_send(h, self._ptr(send), dev))
+                recv = torch.empty(int(wfrom.sum()), dtype=torch.int64, device=self.dev)
+                tdist.all_to_all_single(recv, send, output_split_sizes=[int(x) for x in wfrom],
+                                        input_split_sizes=[int(x) for x in wto], group=self.group)
+                self._done()
+                _check(L.gs_part_xbfs_apply(h, d, self._ptr(recv), wfrom.ctypes.data_as(C.c_void_p), dev,
+                                            C.byref(n)))
+                self.level_bytes += 8 * int(wfrom.sum())
+                tot = torch.tensor([n.value], dtype=torch.int64, device=self.dev)
+                tdist.all_reduce(tot, group=self.group)
+                d += 1
+            _check(L.gs_part_xbfs_end(h))
+            levels = max(levels, d)
+        self.levels = levels
+
     def round(self, round_index, record=False):
         """One iteration of gossip_main.rs:449-564 over the partition."""
         torch, tdist, L, h, dev = self.torch, self.tdist, lib(), self.eng.h, int(self.on_device)
         n = C.c_uint32()
-        _check(L.gs_part_round(h, round_index, int(bool(record)), C.byref(n)))
+        if self.frontier:
+            self._frontier_bfs()
+            _check(L.gs_part_xround_finish(h, round_index, int(bool(record)), C.byref(n)))
+        else:
+            _check(L.gs_part_round(h, round_index, int(bool(record)), C.byref(n)))
         counts = [torch.zeros(1, dtype=torch.int64, device=self.dev) for _ in range(self.world)]
         tdist.all_gather(counts, torch.tensor([n.value], dtype=torch.int64, device=self.dev), group=self.group)
         counts = [int(c.item()) for c in counts]

@@ -63,7 +63,8 @@ enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24
 enum { GS_BFS_AUTO = 0, GS_BFS_WORKGROUP = 1, GS_BFS_LEVEL = 2, GS_BFS_BINNED = 3, GS_BFS_MULTI = 4,
        GS_BFS_HYBRID = 5 };
 enum { GS_FLAG_PROFILE = 1, GS_FLAG_SPLIT_ROUND = 2, GS_FLAG_NARROW_WAVE_PATH = 4, GS_FLAG_BINNED_ALL_LEVELS = 8,
-       GS_FLAG_WIDE_RECORDS = 16, GS_FLAG_NO_SMALL_LEVELS = 32, GS_FLAG_MISPREDICT_LEVELS = 64 };
+       GS_FLAG_WIDE_RECORDS = 16, GS_FLAG_NO_SMALL_LEVELS = 32, GS_FLAG_MISPREDICT_LEVELS = 64,
+       GS_FLAG_FRONTIER_EXCHANGE = 128 };
 
 typedef struct gs_params {
   uint32_t push_fanout;         /* Config::gossip_push_fanout (gossip.rs:113) */
@@ -91,7 +92,10 @@ typedef struct gs_params {
                                    through the grid-wide kernels; same results);
                                    GS_FLAG_MISPREDICT_LEVELS: GS_BFS_BINNED's predicted level loop
                                    inverts its binned/direct choice per level every other round
-                                   (same results; a test of the misprediction path) */
+                                   (same results; a test of the misprediction path);
+                                   GS_FLAG_FRONTIER_EXCHANGE: gs_create_part makes a frontier-exchange
+                                   rank (gs_part_xbfs_*: it expands only its own frontier and
+                                   exchanges each level's push records with their owners) */
 } gs_params;
 
 typedef struct gs_slot {
@@ -237,6 +241,29 @@ int gs_part_prunes_in(gs_engine* e, const void* src, size_t n_records, int src_d
 int gs_part_exchange_sizes(gs_engine* e, size_t* record_cap, size_t* dense_words);
 int gs_part_prunes_dense_out(gs_engine* e, void* dst, int dst_device);           /* [n_nodes][n_slots] u32 */
 int gs_part_prunes_dense_in(gs_engine* e, const void* src, int src_device);
+/* Frontier exchange (params.flags GS_FLAG_FRONTIER_EXCHANGE; SURVEY 8(e), the north star's
+ * "node-range partition with RCCL frontier exchange"). Ranks own whole coarse destination bins
+ * (C = ceil(n / K) rounded up to max(1,024, the multi BFS's coarse bin)); each rank expands
+ * ONLY the frontier entries of its own nodes, and each level's push records go to the rank
+ * owning their destination, which applies them (first arrivals, pool records, its own
+ * next-level entries). For each slot group g < n_groups, the BFS is
+ *   gs_part_xbfs_begin(g, &n)                        seeds the group's own origins; n own entries
+ *   level d = 0, 1, ... while the SUM of n over ranks > 0:
+ *     gs_part_xbfs_expand(d, words_to[K])            expand own entries, pack per owner rank
+ *     ALL-TO-ALL the K counts, then gs_part_xbfs_send(buf) -> ALL-TO-ALL (split by words_to /
+ *       words_from, u64 words: per message the owner's bin counts, then the records)
+ *     gs_part_xbfs_apply(d, recv, words_from[K], &n)  apply what every rank pushed here
+ *   gs_part_xbfs_end()                               the group's in-degrees, hops, inbound rows
+ * then gs_part_xround_finish(round, record, &n_records) (consume + send_prunes of own nodes)
+ * in place of gs_part_round; the prune and statistics exchanges follow as above. */
+int gs_part_xbfs_groups(gs_engine* e, uint32_t* n_groups);
+int gs_part_xbfs_begin(gs_engine* e, uint32_t group, uint32_t* n_local);
+int gs_part_xbfs_expand(gs_engine* e, uint32_t level, uint64_t* words_to /*[K]*/);
+int gs_part_xbfs_send(gs_engine* e, void* dst, int dst_device);
+int gs_part_xbfs_apply(gs_engine* e, uint32_t level, const void* src, const uint64_t* words_from /*[K]*/,
+                       int src_device, uint32_t* n_local);
+int gs_part_xbfs_end(gs_engine* e);
+int gs_part_xround_finish(gs_engine* e, uint32_t round, int record, uint32_t* n_records);
 int gs_part_stats_out(gs_engine* e, void* dst, int dst_device);          /* [S][5 + 256 + W] u64 */
 int gs_part_stats_in(gs_engine* e, const void* src, int src_device);
 

@@ -1,6 +1,7 @@
 """One rank of a node-range-partitioned run (tests/test_partition.py). Env: RANK,
 WORLD_SIZE, MASTER_ADDR/PORT, GS_PART_OUT (npz path), GS_PART_CASE (small | large),
-GS_PART_BACKEND (gloo | nccl)."""
+GS_PART_BACKEND (gloo | nccl), GS_PART_EXCHANGE (prune exchange: auto | records | dense),
+GS_PART_BFS (replicated | frontier)."""
 import os
 import pickle
 import sys
@@ -37,7 +38,8 @@ def main():
     st = stakes_of(case, eb.synth)
     pe = gp.PartitionedEngine(st, len(CASES[case]["mi"]), device=0, seed=CASES[case]["seed"],
                               rotation_probability=CASES[case]["p"],
-                              exchange=os.environ.get("GS_PART_EXCHANGE", "auto"))
+                              exchange=os.environ.get("GS_PART_EXCHANGE", "auto"),
+                              bfs=os.environ.get("GS_PART_BFS", "replicated"))
     modes = []
     out = run_case(pe, case, st, ranges=[(pe.node_lo, pe.node_hi)],
                    on_round=lambda r, e: modes.append((r, e.last_mode or "", e.records)))
@@ -45,6 +47,7 @@ def main():
     out["xmodes"] = np.array([m for _, m, _ in modes])
     out["xrecords"] = np.array([n for _, _, n in modes], dtype=np.uint64)
     out["xbytes"] = np.array([pe.bytes_in], dtype=np.uint64)
+    out["levels"] = np.array([pe.levels, pe.level_bytes], dtype=np.uint64)
     info = pe.info()
     out["bytes"] = np.array([info["device_bytes"], info["pair_bytes"], info["other_bytes"]], dtype=np.uint64)
     np.savez(os.environ["GS_PART_OUT"], **out)

@@ -2,7 +2,8 @@
 engine's multi-GPU paths over the backend GS_RCCL_BACKEND (nccl = RCCL on ROCm, or gloo),
 world size 1 on cuda:0. Writes the results to GS_RCCL_OUT (npz):
   part_<exchange>_*  the node-range partition's small case (PartitionedEngine: prune
-                     records / dense words and statistics through device buffers)
+                     records / dense words and statistics through device buffers; part_frontier_*:
+                     the frontier-exchange BFS's per-level all-to-alls on device buffers)
   sweep_*            a sharded fail-nodes sweep (sweep.run_sharded -> allreduce_results)
   rows               sweep.gather_rows of a byte matrix (the origin-shard reassembly)"""
 import os
@@ -28,9 +29,9 @@ def main():
     out = {}
     st = stakes_of("small", eb.synth)
     c = CASES["small"]
-    for exchange in ("records", "dense"):
+    for exchange, bfs in (("records", "replicated"), ("dense", "replicated"), ("frontier", "frontier")):
         pe = gp.PartitionedEngine(st, len(c["mi"]), device=0, seed=c["seed"], rotation_probability=c["p"],
-                                  exchange=exchange)
+                                  exchange="auto" if bfs == "frontier" else exchange, bfs=bfs)
         modes = []
         res = run_case(pe, "small", st, on_round=lambda r, e: modes.append(e.last_mode or ""))
         assert pe.on_device == (backend == "nccl")

@@ -31,13 +31,13 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(tmp_path, case, backend, world=2, exchange="auto", extra_env=None):
+def run_ranks(tmp_path, case, backend, world=2, exchange="auto", extra_env=None, bfs="replicated"):
     port = free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), GS_PART_OUT=str(tmp_path / f"rank{r}.npz"), GS_PART_CASE=case,
-                   GS_PART_BACKEND=backend, GS_PART_EXCHANGE=exchange, **(extra_env or {}))
+                   GS_PART_BACKEND=backend, GS_PART_EXCHANGE=exchange, GS_PART_BFS=bfs, **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "partition_worker.py")], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     try:
@@ -69,14 +69,31 @@ def test_partition_ranges_refuse_empty_ranks():
         gp.partition_ranges(3000, 4)  # ranges of 1,024: the fourth rank would start at 3,072
 
 
+def test_partition_ranges_frontier_units():
+    """A frontier-exchange partition owns whole coarse bins of the multi BFS (mv_geometry's
+    ~256 bins of 2^6 .. 2^13 nodes), at least 1,024 ids."""
+    import gossip_sim_amd.partition as gp
+    assert gp.coarse_bin_nodes(3000) == 64 and gp.coarse_bin_nodes(1_000_000) == 4096
+    assert gp.coarse_bin_nodes(10_000_000) == 8192
+    assert gp.partition_ranges(3000, 2, frontier=True) == [(0, 2048), (2048, 3000)]
+    assert gp.partition_ranges(1_000_000, 2, frontier=True) == [(0, 503808), (503808, 1_000_000)]
+    assert all(lo % 8192 == 0 for lo, _ in gp.partition_ranges(10_000_000, 8, frontier=True))
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("case,backend,exchange", [
-    ("small", "gloo", "auto"), ("small", "gloo", "dense"), ("small", "nccl", "auto"),
-    ("large", "gloo", "auto"), ("large", "gloo", "records")])
-def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend, exchange):
-    """(exchange: auto = records outside prune waves, dense in them; records / dense forced.)"""
+@pytest.mark.parametrize("case,backend,exchange,bfs", [
+    ("small", "gloo", "auto", "replicated"), ("small", "gloo", "dense", "replicated"),
+    ("small", "nccl", "auto", "replicated"), ("large", "gloo", "auto", "replicated"),
+    ("large", "gloo", "records", "replicated"),
+    ("small", "gloo", "auto", "frontier"), ("large", "gloo", "auto", "frontier")])
+def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend, exchange, bfs):
+    """(exchange: the prune exchange -- auto = records outside prune waves, dense in them;
+    records / dense forced. bfs: replicated = every rank runs the whole BFS; frontier = each
+    rank expands its own frontier and the level's push records go to their owners.)"""
     extra = {"GS_PART_RECORD_CAP": str(1 << 25)} if exchange == "records" else None
-    parts, caches = run_ranks(tmp_path, case, backend, exchange=exchange, extra_env=extra)
+    parts, caches = run_ranks(tmp_path, case, backend, exchange=exchange, extra_env=extra, bfs=bfs)
+    if bfs == "frontier":
+        assert all(int(p["levels"][0]) >= 3 and int(p["levels"][1]) > 0 for p in parts), [p["levels"] for p in parts]
     modes = set(str(m) for m in parts[0]["xmodes"] if str(m))
     if exchange != "auto":
         assert modes == {exchange}, modes
@@ -104,7 +121,7 @@ def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend, exchang
                 np.testing.assert_array_equal(p[f"cache{k}"][lo:hi], want[f"cache{k}"][lo:hi], err_msg=f"cache {k}")
             for v, row in caches[r][k].items():
                 assert row == want_caches[k][v], f"cache slot {k} node {v}"
-    if case == "large" and exchange == "auto":
+    if case == "large" and exchange == "auto" and bfs == "replicated":
         # device memory per rank: its share of the per-(slot, node) state + the replicated tables
         # (the forced-records run enlarges the record buffer by GS_PART_RECORD_CAP: not compared)
         full = eb.gs.Engine(st, S, bfs_mode=eb.gs.GS_BFS_MULTI, seed=c["seed"], rotation_probability=c["p"])

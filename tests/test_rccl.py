@@ -5,7 +5,8 @@ group, and compared bit for bit with the same run over gloo and with one plain e
 RCCL refuses two ranks on one GPU (tests/test_partition.py skips its nccl case for that),
 but a one-rank communicator runs every collective for real on device buffers: the node
 partition's prune-record all-gather and dense-word all-reduce read and written by
-gs_part_prunes_out/_in and gs_part_prunes_dense_out/_in with dev = 1, its statistics
+gs_part_prunes_out/_in and gs_part_prunes_dense_out/_in with dev = 1, the frontier-exchange
+BFS's two all-to-alls per level (gs_part_xbfs_send / _apply with dev = 1), its statistics
 all-reduce (gs_part_stats_out/_in), the sweep assembly (sweep.allreduce_results on
 cuda:0) and the origin-shard reassembly (sweep.gather_rows). The reference's finalize
 step these replace: gossip_main.rs:567-646."""
@@ -57,7 +58,7 @@ def test_rccl_world1_exchanges_match_gloo_and_one_engine(tmp_path):
     want = run_case(one, "small", st)
     one.close()
     assert want["summaries"]["prunes"].sum() > 0
-    for ex in ("records", "dense"):
+    for ex in ("records", "dense", "frontier"):
         for k, v in want.items():
             got = nccl[f"part_{ex}_{k}"]
             assert got.tobytes() == np.asarray(v).tobytes(), (ex, k)
