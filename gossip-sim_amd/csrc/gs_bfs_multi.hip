@@ -1681,9 +1681,12 @@ hipError_t mvx_apply(Engine& e, uint32_t g, uint32_t d, const unsigned long long
   return hipGetLastError();
 }
 
-hipError_t mvx_gather(Engine& e, uint32_t g) {
+// After the group's last level: gather + consume of its own nodes straight from the LDS CSR
+// (k_mv_consume, as the replicated partition's round; no inbound rows are written).
+hipError_t mvx_gather_consume(Engine& e, uint32_t g, bool record) {
   MvArgs a = mv_args(e, e.mv_groups[g], g);
-  hipLaunchKernelGGL(k_mv_gather, dim3(mv_kept_bins(e)), dim3(MV_GT), mv_glds(), e.st, a);
+  a.record = record ? 1u : 0u;
+  hipLaunchKernelGGL(k_mv_consume, dim3(mv_kept_bins(e)), dim3(MV_GT), mv_glds(), e.st, a);
   return hipGetLastError();
 }
 

@@ -1382,7 +1382,6 @@ int gs_part_xbfs_begin(gs_engine* eh, uint32_t group, uint32_t* n_local) {
   if (int s = need_slots(e)) return s;
   if (!n_local || group >= e->mv_groups.size()) return fail(GS_EINVAL, "bad group / null argument");
   if (int s = flush_rot_clear(e)) return s;
-  if (int s = ensure_inb(e)) return s;
   if (group == 0) HIPC(hipMemsetAsync(e->part_cnt, 0, 4, e->st));
   e->x_group = group;
   e->x_level = 0;
@@ -1445,16 +1444,16 @@ int gs_part_xbfs_apply(gs_engine* eh, uint32_t level, const void* src, const uin
   return check_err(e);
 }
 
-int gs_part_xbfs_end(gs_engine* eh) {
+int gs_part_xbfs_end(gs_engine* eh, int record) {
   PARTX(eh);
   if (e->x_group == 0xFFFFFFFFu) return fail(GS_ESTATE, "gs_part_xbfs_end: no group begun");
   e->tend("bfs", e->x_t0);
   hipEvent_t t0;
-  e->tbegin("gather", &t0);
-  HIPC(mvx_gather(*e, e->x_group));
-  e->tend("gather", t0);
+  e->tbegin("gather_consume", &t0);
+  HIPC(mvx_gather_consume(*e, e->x_group, record != 0));
+  e->tend("gather_consume", t0);
   e->x_group = 0xFFFFFFFFu;
-  e->inb_valid = true;
+  e->inb_valid = false;
   return check_err(e);
 }
 
@@ -1466,7 +1465,7 @@ int gs_part_xround_finish(gs_engine* eh, uint32_t round, int record, uint32_t* n
   hipEvent_t t0;
   e->tbegin("consume", &t0);
   hipError_t r = hipMemsetAsync(e->slot_prunes, 0, e->S * 4, e->st);
-  if (r == hipSuccess) r = launch_consume_prune_g(*e, rec, true);  // consume + send_prunes of own nodes
+  if (r == hipSuccess) r = launch_consume_prune_g(*e, rec, false);  // send_prunes of own pruners (consumed at xbfs_end)
   if (r == hipSuccess) r = launch_part_emit(*e);                   // ... as records for the other ranks
   e->tend("consume", t0);
   HIPC(r);

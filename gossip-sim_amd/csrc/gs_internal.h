@@ -291,7 +291,7 @@ hipError_t mvx_begin(Engine& e, uint32_t g, uint32_t& n_local);
 hipError_t mvx_expand(Engine& e, uint32_t g, uint32_t d, uint32_t n_local, std::vector<uint64_t>& words_to);
 hipError_t mvx_apply(Engine& e, uint32_t g, uint32_t d, const unsigned long long* recv,
                      const std::vector<uint64_t>& words_from, uint32_t& n_next);
-hipError_t mvx_gather(Engine& e, uint32_t g);
+hipError_t mvx_gather_consume(Engine& e, uint32_t g, bool record);
 // own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);

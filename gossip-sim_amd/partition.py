@@ -132,11 +132,12 @@ class PartitionedEngine:
         if self.on_device:
             self.torch.cuda.synchronize()
 
-    def _frontier_bfs(self):
+    def _frontier_bfs(self, record):
         """Cluster::run_gossip (gossip.rs:494-615) over the partition with a frontier exchange
         per level: each rank expands only its own frontier entries; the level's push records
         go to the ranks owning their destinations (two all-to-alls: the counts, then the
-        messages), which apply them; the BFS ends when no rank has a next-level entry."""
+        messages), which apply them; the BFS ends when no rank has a next-level entry. Each
+        group's own nodes are then gathered and consumed (consume_messages, gossip.rs:618-653)."""
         torch, tdist, L, h, dev = self.torch, self.tdist, lib(), self.eng.h, int(self.on_device)
         K = self.world
         ng = C.c_uint32()
@@ -168,7 +169,7 @@ class PartitionedEngine:
                 tot = torch.tensor([n.value], dtype=torch.int64, device=self.dev)
                 tdist.all_reduce(tot, group=self.group)
                 d += 1
-            _check(L.gs_part_xbfs_end(h))
+            _check(L.gs_part_xbfs_end(h, int(bool(record))))
             levels = max(levels, d)
         self.levels = levels
 
@@ -177,7 +178,7 @@ class PartitionedEngine:
         torch, tdist, L, h, dev = self.torch, self.tdist, lib(), self.eng.h, int(self.on_device)
         n = C.c_uint32()
         if self.frontier:
-            self._frontier_bfs()
+            self._frontier_bfs(record)
             _check(L.gs_part_xround_finish(h, round_index, int(bool(record)), C.byref(n)))
         else:
             _check(L.gs_part_round(h, round_index, int(bool(record)), C.byref(n)))

@@ -253,8 +253,8 @@ int gs_part_prunes_dense_in(gs_engine* e, const void* src, int src_device);
  *     ALL-TO-ALL the K counts, then gs_part_xbfs_send(buf) -> ALL-TO-ALL (split by words_to /
  *       words_from, u64 words: per message the owner's bin counts, then the records)
  *     gs_part_xbfs_apply(d, recv, words_from[K], &n)  apply what every rank pushed here
- *   gs_part_xbfs_end()                               the group's in-degrees, hops, inbound rows
- * then gs_part_xround_finish(round, record, &n_records) (consume + send_prunes of own nodes)
+ *   gs_part_xbfs_end(record)                         gather + consume_messages of the group's own nodes
+ * then gs_part_xround_finish(round, record, &n_records) (send_prunes of own pruners)
  * in place of gs_part_round; the prune and statistics exchanges follow as above. */
 int gs_part_xbfs_groups(gs_engine* e, uint32_t* n_groups);
 int gs_part_xbfs_begin(gs_engine* e, uint32_t group, uint32_t* n_local);
@@ -262,7 +262,7 @@ int gs_part_xbfs_expand(gs_engine* e, uint32_t level, uint64_t* words_to /*[K]*/
 int gs_part_xbfs_send(gs_engine* e, void* dst, int dst_device);
 int gs_part_xbfs_apply(gs_engine* e, uint32_t level, const void* src, const uint64_t* words_from /*[K]*/,
                        int src_device, uint32_t* n_local);
-int gs_part_xbfs_end(gs_engine* e);
+int gs_part_xbfs_end(gs_engine* e, int record);
 int gs_part_xround_finish(gs_engine* e, uint32_t round, int record, uint32_t* n_records);
 int gs_part_stats_out(gs_engine* e, void* dst, int dst_device);          /* [S][5 + 256 + W] u64 */
 int gs_part_stats_in(gs_engine* e, const void* src, int src_device);

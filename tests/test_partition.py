@@ -136,16 +136,18 @@ def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend, exchang
 
 
 @pytest.mark.gpu
-def test_partition_c5_as_configured(tmp_path):
+@pytest.mark.parametrize("bfs", ["replicated", "frontier"])
+def test_partition_c5_as_configured(tmp_path, bfs):
     """BASELINE C5 as configured on the box's one GPU: 10M nodes, origin ranks 1..16 as 16
     slots, node-range partitioned over two gloo ranks (two engines on device 0), 22 rounds
     through the first prune wave (records exchanged in ordinary rounds, dense words in the
     wave). Equals one unpartitioned engine (the level-synchronous BFS) bit for bit: every
     per-round summary and hop histogram, per-rank digests of owned hops and accumulators,
     the replicated prune state, sampled caches; and the size-independent BFS properties
-    hold on the unpartitioned run."""
+    hold on the unpartitioned run. bfs="frontier": each rank expands only its own frontier and
+    the levels' push records go to their owners (the north star's frontier exchange)."""
     from test_gpu_parity import _invariants
-    parts, caches = run_ranks(tmp_path, "c5", "gloo")
+    parts, caches = run_ranks(tmp_path, "c5", "gloo", bfs=bfs)
     c = CASES["c5"]
     n, S = c["n"], len(c["mi"])
     ranges = [(int(p["lo"][0]), int(p["hi"][0])) for p in parts]
