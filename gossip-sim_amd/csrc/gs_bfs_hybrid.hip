@@ -136,11 +136,10 @@ __global__ __launch_bounds__(XT) void k_hb_graph(MvArgs a) {
       const size_t b64 = rw * XT * a.ASZ;
       const bool ok = b64 + total <= a.area_cap;
       if (!ok && tid == 0) atomicOr(a.err, ERR_MV_CAP | ERR_MVD_AREA);
-      uint32_t* Tr = a.T + rw * a.TW;
-      for (uint32_t b = tid; b < nb; b += XT) Tr[1 + b] = ok ? hist[b] : 0u;
+      for (uint32_t b = tid; b < nb; b += XT) mv_t(a, (uint32_t)rw, 1 + b) = ok ? hist[b] : 0u;
       if (tid == 0) {
-        Tr[0] = ok ? (uint32_t)b64 : 0u;
-        Tr[1 + nb] = ok ? total : 0u;
+        mv_t(a, (uint32_t)rw, 0) = ok ? (uint32_t)b64 : 0u;
+        mv_t(a, (uint32_t)rw, 1 + nb) = ok ? total : 0u;
       }
 #pragma unroll
       for (int s = 0; s < ASZP; ++s)
@@ -207,10 +206,9 @@ __global__ __launch_bounds__(HB_CT) void k_hb_csr(MvArgs a) {
     for (uint32_t c0 = 0; c0 < R; c0 += MV_SEG) {
       const uint32_t gc = min(MV_SEG, R - c0);
       for (uint32_t i = tid; i < gc; i += HB_CT) {
-        const uint32_t* Tr = a.T + (size_t)(c0 + i) * a.TW;
-        const uint32_t st = Tr[1 + c];
-        pre[i] = Tr[2 + c] - st;
-        sb[i] = Tr[0] + st;
+        const uint32_t st = mv_t(a, c0 + i, 1 + c);
+        pre[i] = mv_t(a, c0 + i, 2 + c) - st;
+        sb[i] = mv_t(a, c0 + i, 0) + st;
       }
       __syncthreads();
       const uint32_t ct = mv_block_scan(pre, gc, ctl);

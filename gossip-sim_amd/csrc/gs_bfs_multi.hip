@@ -106,11 +106,10 @@ __global__ __launch_bounds__(XT) void k_mv_expand(MvArgs a, uint32_t d, uint32_t
     __syncthreads();
     const uint32_t base = sbase;
     const bool ok = base != 0xFFFFFFFFu;
-    uint32_t* Tr = a.T + (size_t)w * a.TW;
-    for (uint32_t b = tid; b < nb; b += XT) Tr[1 + b] = ok ? hist[b] : 0u;
+    for (uint32_t b = tid; b < nb; b += XT) mv_t(a, w, 1 + b) = ok ? hist[b] : 0u;
     if (tid == 0) {
-      Tr[0] = ok ? base : 0u;
-      Tr[1 + nb] = ok ? total : 0u;
+      mv_t(a, w, 0) = ok ? base : 0u;
+      mv_t(a, w, 1 + nb) = ok ? total : 0u;
     }
 #pragma unroll
     for (int s = 0; s < ASZP; ++s)
@@ -176,10 +175,9 @@ __global__ __launch_bounds__(MV_AT) void k_mv_apply(MvArgs a, uint32_t d, uint32
   for (uint32_t c0 = 0; c0 < G; c0 += MV_SEG) {
     const uint32_t gc = min(MV_SEG, G - c0);
     for (uint32_t i = tid; i < gc; i += MV_AT) {
-      const uint32_t* Tr = a.T + (size_t)(c0 + i) * a.TW;
-      const uint32_t st = Tr[1 + c];
-      pre[i] = Tr[2 + c] - st;  // bin starts are exclusive; Tr[1 + nbc] is the run's total
-      sb[i] = Tr[0] + st;
+      const uint32_t st = mv_t(a, c0 + i, 1 + c);
+      pre[i] = mv_t(a, c0 + i, 2 + c) - st;  // bin starts are exclusive; entry 1 + nbc is the run's total
+      sb[i] = mv_t(a, c0 + i, 0) + st;
     }
     __syncthreads();
     const uint32_t ct = mv_block_scan(pre, gc, ctl);
@@ -1072,8 +1070,7 @@ __global__ __launch_bounds__(256) void k_mvx_bincount(MvArgs a, uint32_t G, uint
   const uint32_t c = blockIdx.x;
   uint32_t s = 0;
   for (uint32_t i = threadIdx.x; i < G; i += 256) {
-    const uint32_t* Tr = a.T + (size_t)i * a.TW;
-    s += Tr[2 + c] - Tr[1 + c];
+    s += mv_t(a, i, 2 + c) - mv_t(a, i, 1 + c);
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
@@ -1095,10 +1092,9 @@ __global__ __launch_bounds__(256) void k_mvx_pack(MvArgs a, uint32_t G, const un
   for (uint32_t c0 = 0; c0 < G; c0 += MV_SEG) {
     const uint32_t gc = min(MV_SEG, G - c0);
     for (uint32_t i = tid; i < gc; i += 256) {
-      const uint32_t* Tr = a.T + (size_t)(c0 + i) * a.TW;
-      const uint32_t st = Tr[1 + c];
-      pre[i] = Tr[2 + c] - st;
-      sb[i] = Tr[0] + st;
+      const uint32_t st = mv_t(a, c0 + i, 1 + c);
+      pre[i] = mv_t(a, c0 + i, 2 + c) - st;
+      sb[i] = mv_t(a, c0 + i, 0) + st;
     }
     __syncthreads();
     const uint32_t ct = mv_block_scan(pre, gc, wsum);
@@ -1117,23 +1113,23 @@ __global__ __launch_bounds__(256) void k_mvx_pack(MvArgs a, uint32_t G, const un
   }
 }
 
-// T row q of a received level: sender q's message (words off[q] ..) is nbm header words
-// (record counts of this rank's bins blo, blo + 1, ...) then the records, bin by bin.
+// T row q of a received level (bin-major with stride K, as mv_t): sender q's message (words
+// off[q] ..) is nbm header words (record counts of this rank's bins blo, blo + 1, ...) then the
+// records, bin by bin.
 __global__ __launch_bounds__(64) void k_mvx_trows(const unsigned long long* __restrict__ recv,
                                                   const unsigned long long* __restrict__ off, uint32_t blo, uint32_t nbm,
-                                                  uint32_t nbc, uint32_t TW, uint32_t* __restrict__ T) {
+                                                  uint32_t nbc, uint32_t K, uint32_t* __restrict__ T) {
   const uint32_t q = blockIdx.x;
-  uint32_t* Tr = T + (size_t)q * TW;
   const unsigned long long o = off[q];
-  for (uint32_t b = threadIdx.x; b < blo; b += 64) Tr[1 + b] = 0;
+  for (uint32_t b = threadIdx.x; b < blo; b += 64) T[(size_t)(1 + b) * K + q] = 0;
   if (threadIdx.x == 0) {
-    Tr[0] = (uint32_t)(o + nbm);
+    T[q] = (uint32_t)(o + nbm);
     uint32_t run = 0;
     for (uint32_t i = 0; i < nbm; ++i) {
-      Tr[1 + blo + i] = run;
+      T[(size_t)(1 + blo + i) * K + q] = run;
       run += (uint32_t)recv[o + i];
     }
-    for (uint32_t b = blo + nbm; b <= nbc; ++b) Tr[1 + b] = run;
+    for (uint32_t b = blo + nbm; b <= nbc; ++b) T[(size_t)(1 + b) * K + q] = run;
   }
 }
 
@@ -1297,6 +1293,7 @@ MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.pool = e.mv_pool; a.pused = e.mv_pused;
   a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
+  a.TS = (uint32_t)e.mv.rows_cap;
   a.vlo = e.vlo; a.vhi = e.vlo + e.NP; a.NP = e.NP; a.MSU = (uint32_t)e.msu;
   a.XT = e.mv.XT;
   a.xrows = 0;
@@ -1553,8 +1550,14 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
       while (k1 > k0 && pv[k1 - 1] <= tail_thr) --k1;
       const uint32_t npairs = std::min<uint32_t>(k1 - k0 + mv_margin(), 250);
       launch_small_levels(e, a, MV_HEAD, 0u, 0u, e.mv_seed + gr.seed0, gr.nseed, 0u, lds_s);
+      static const bool full_grid = std::getenv("GS_MV_XGRID_FULL") && std::getenv("GS_MV_XGRID_FULL")[0] == '1';
       for (uint32_t i = 0; i < npairs; ++i) {
-        launch_expand(e, a, 0u, i, lds_x, xgrid);
+        // the pair's expand grid from the predicted level (+25 %; slices beyond it are taken by
+        // the grid-stride loop): small levels launch a few workgroups instead of 2,048
+        const uint32_t pl = k0 + i < pv.size() ? pv[k0 + i] : 0u;
+        const uint32_t gp = (uint32_t)(((size_t)pl + e.mv.XT - 1) / e.mv.XT);
+        const uint32_t xg = full_grid ? xgrid : std::min<uint32_t>(xgrid, std::max<uint32_t>(16, gp + gp / 4 + 8));
+        launch_expand(e, a, 0u, i, lds_x, xg);
         hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, 0u, i, e.mv_q[0], e.mv_q[1]);
       }
       const uint32_t seq = ++e.mv_seq ? e.mv_seq : ++e.mv_seq;  // (never 0)
@@ -1668,8 +1671,9 @@ hipError_t mvx_apply(Engine& e, uint32_t g, uint32_t d, const unsigned long long
   uint32_t blo, nbm;
   mvx_bins(e, e.part_rank, blo, nbm);
   if ((r = hipMemcpyAsync(e.x_off, off.data(), (K + 1) * 8, hipMemcpyHostToDevice, e.st))) return r;
-  hipLaunchKernelGGL(k_mvx_trows, dim3(K), dim3(64), 0, e.st, recv, e.x_off, blo, nbm, e.mv.nbc, e.mv.TW, e.x_T);
+  hipLaunchKernelGGL(k_mvx_trows, dim3(K), dim3(64), 0, e.st, recv, e.x_off, blo, nbm, e.mv.nbc, K, e.x_T);
   a.T = e.x_T;
+  a.TS = K;
   a.area = const_cast<unsigned long long*>(recv);
   a.xrows = K;
   const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);

@@ -59,6 +59,7 @@ struct MvArgs {
   uint32_t XT;   // frontier entries per expand slice (MV_XT or MV_XT_L; mv_geometry)
   uint32_t small;  // levels of at most this many entries run in the one-workgroup kernel
   uint32_t xrows;  // frontier-exchange partition: apply walks this many T rows (one per sender rank), else 0
+  uint32_t TS;     // T: entries of one bin slot for consecutive runs are TS apart (mv_t)
   size_t PAIRS, area_cap, rows_cap, q_cap, pcap;
   // direction-optimizing BFS over the round's push graph (gs_bfs_hybrid.hip)
   uint8_t* dist;              // [N][DSP] each slot's BFS distance (0xFF: not reached)
@@ -71,6 +72,13 @@ struct MvArgs {
   uint32_t pg_slices;         // push-graph slices (XT nodes each)
   uint32_t bu_min;            // bottom-up level: predicted entries at least (host side)
 };
+
+// Entry b of expand run (T row) w: b = 0 the run's base in the record area, b = 1 + c its
+// start of coarse bin c, b = 1 + nbc its total. Stored bin-major, T[b * TS + w]: an apply
+// workgroup reads its bin's starts over every run of the level as one contiguous range
+// (row-major it read one scattered word per run: at C5's thousands of runs per level the
+// column walk streamed ~1 GB of lines per peak level through L2).
+__device__ inline uint32_t& mv_t(const MvArgs& a, uint32_t w, uint32_t b) { return a.T[(size_t)b * a.TS + w]; }
 
 // A pool record: src | node-in-fine-bin << UB | hop << (UB + BSF) | slot mask << (UB + BSF + 8)
 // (mv_geometry keeps UB + BSF + 8 + GW <= 64). The hop travels with the record, so the
