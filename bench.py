@@ -364,6 +364,8 @@ def sweep_workload(gs, synth, args, rank, world, dev, barrier, reduce):
     value = all ranks' pushes / the slowest rank's time."""
     import numpy as np
     kind = args.workload
+    if kind == "c3":
+        return c3_sweep_workload(gs, synth, args, rank, world, dev, barrier, reduce)
     if kind == "c4":
         nodes = 1_000_000
         stakes = synth.power_law_stakes(nodes)
@@ -434,6 +436,67 @@ def sweep_workload(gs, synth, args, rank, world, dev, barrier, reduce):
             "origin_rounds_per_s": sims_total * args.steps / dt, "roofline_rank0": roof, "cpu_baseline": None}
 
 
+def c3_sweep_workload(gs, synth, args, rank, world, dev, barrier, reduce):
+    """--workload c3: BASELINE C3 -- the 100k-node network's active-set-size sweep
+    (num-simulations 16, step 1: active-set sizes 12..27, gossip_main.rs:774-800), sims dealt
+    round-robin over the ranks (strong: the total work is fixed) or all 16 on every rank with
+    Philox seed + rank (weak). Each sim has its own active sets, so each is one engine of one
+    slot; a rank runs its engines concurrently (one host thread and stream each)."""
+    import threading
+    import numpy as np
+    nodes = 100_000
+    stakes = synth.power_law_stakes(nodes)
+    origin = int(np.argmax(stakes))
+    sizes = [12 + i for i in range(16)]
+    weak = args.scaling == "weak"
+    mine = sizes if weak else sizes[rank::world]
+    seed = args.seed + rank if weak else args.seed
+    engs = []
+    for asz in mine:
+        e = gs.Engine(stakes, 1, fanout=args.fanout, active_set_size=asz, rotation_probability=0.013333, seed=seed,
+                      device=dev, profile=True, bfs_mode=args.large_mode)
+        e.set_slots([origin], args.min_ingress, args.threshold)
+        e.init_active_sets()
+        engs.append((asz, e))
+
+    def run(e, r0, r1, rec):
+        for r in range(r0, r1):
+            e.round(r, record=rec)
+        e.sync()
+
+    def all_engines(r0, r1, rec):
+        th = [threading.Thread(target=run, args=(e, r0, r1, rec)) for _, e in engs]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+
+    all_engines(0, args.warmup, False)
+    for _, e in engs:
+        e.kernel_time_reset()
+    barrier()
+    t0 = time.perf_counter()
+    all_engines(args.warmup, args.warmup + args.steps, True)
+    barrier()
+    dt = reduce(time.perf_counter() - t0, lambda d: d.ReduceOp.MAX)
+    E = 0.0
+    for _, e in engs:
+        E += float(e.summaries()["pushes"].astype("float64").sum())
+        e.close()
+    E_all = reduce(E, lambda d: d.ReduceOp.SUM)
+    sims_total = 16 * (world if weak else 1)
+    return {"metric": METRIC, "value": E_all / dt, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (deterministic Philox power-law stakes, SURVEY.md 8(d))",
+            "config": {"workload": "C3: 100k-node power-law network, active-set-size sweep 12..27 (16 sims)" +
+                                   (" per rank, rank r = Philox seed + r" if weak else " dealt round-robin over the ranks"),
+                       "nodes": nodes, "sims_total": sims_total, "sims_rank0": len(mine),
+                       "active_set_sizes_rank0": mine, "rounds": [args.warmup, args.warmup + args.steps],
+                       "parallelism": (f"trial-sharded x{world}" if weak else f"sweep-sharded x{world} (one network)")},
+            "origin_rounds_per_s": sims_total * args.steps / dt, "cpu_baseline": None}
+
+
 # ------------------------------------------------------------------------ main ----
 def main():
     ap = argparse.ArgumentParser()
@@ -467,9 +530,10 @@ def main():
     ap.add_argument("--per-rank-networks", action="store_true", help="= --scaling weak")
     ap.add_argument("--check-shard", action="store_true",
                     help="with origin sharding: rank 0 re-runs all origins on one engine and compares")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"],
-                    help="c4: BASELINE C4's 13 sims (1M nodes), c5: C5's 16 origins (10M nodes) over the ranks "
-                         "(--scaling strong: dealt round-robin; weak: every rank all of them, seed + rank)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
+                    help="c3: BASELINE C3's 16-sim active-set-size sweep (100k nodes), c4: C4's 13 sims (1M nodes), "
+                         "c5: C5's 16 origins (10M nodes) over the ranks (--scaling strong: dealt round-robin; weak: "
+                         "every rank all of them, seed + rank)")
     args = ap.parse_args()
     if args.shard_origins:
         args.scaling = "strong"
@@ -513,7 +577,7 @@ def main():
         dist[1].all_reduce(t, op=op(dist[1]))
         return float(t.item())
 
-    if args.workload in ("c4", "c5"):
+    if args.workload in ("c3", "c4", "c5"):
         out = sweep_workload(gs, synth, args, rank, world, dev, barrier, reduce)
         if rank == 0:
             print(json.dumps(out), flush=True)
@@ -531,9 +595,14 @@ def main():
     else:
         origins, seed = all_origins, args.seed + rank
     S = len(origins)
+    # (the headline times only the round kernel: an event pair at every family boundary idles
+    # the GPU a few us; GS_PROFILE_ONLY is read at engine creation)
+    os.environ.setdefault("GS_PROFILE_ONLY", "round,bfs")
     eng = gs.Engine(stakes, S, fanout=args.fanout, active_set_size=args.active_set_size,
                     rotation_probability=args.rotation_probability, seed=seed, device=dev,
                     bfs_mode=args.bfs_mode, profile=not args.no_profile, split_round=args.split_round)
+    if os.environ.get("GS_PROFILE_ONLY") == "round,bfs":
+        del os.environ["GS_PROFILE_ONLY"]  # (the legs' engines time every family)
     eng.set_slots(origins, args.min_ingress, args.threshold)
     eng.init_active_sets()
     for r in range(args.warmup):

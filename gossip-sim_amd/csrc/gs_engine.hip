@@ -39,9 +39,16 @@ hipEvent_t Engine::ev_take() {
   }
   return x;
 }
+// GS_PROFILE_ONLY=fam1,fam2 at gs_create: this engine times only these families (an event
+// record at a family boundary idles the GPU for a few us; bench.py's headline reads only the
+// round kernel's)
+static bool family_timed(const Engine& e, const char* fam) {
+  return e.prof_only.empty() || e.prof_only.find("," + std::string(fam) + ",") != std::string::npos;
+}
+
 void Engine::tbegin(const char* fam, hipEvent_t* a) {
   *a = nullptr;
-  if (!(prm.flags & GS_FLAG_PROFILE)) return;
+  if (!(prm.flags & GS_FLAG_PROFILE) || !family_timed(*this, fam)) return;
   *a = ev_take();
   hipEventRecord(*a, st);
   (void)fam;
@@ -234,6 +241,7 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   Engine* e = new (std::nothrow) Engine();
   if (!e) return fail(GS_ENOMEM, "host allocation");
   e->prm = *prm;
+  if (const char* x = std::getenv("GS_PROFILE_ONLY")) e->prof_only = "," + std::string(x) + ",";
   e->N = n;
   e->S = n_slots;
   e->NP = n;
@@ -288,11 +296,12 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     e->vlo = lo;
     e->PAIRS = (size_t)e->NP * n_slots;
   }
-  // AUTO, measured: MULTI 2.6 vs BINNED 3.6 ms per C4 round (13 slots); BINNED ahead at 1
-  // slot; at 10M nodes (1,024-entry expand slices) MULTI already wins at 2 slots (4.86 vs 5.26 ms)
+  // AUTO, measured: MULTI 2.6 vs BINNED 3.6 ms per C4 round (13 slots); at 10M nodes MULTI wins
+  // from 2 slots (4.86 vs 5.26 ms); round 5, with expand grids sized from the level profile, at
+  // one slot too (C3's one-slot 100k engines: 0.371 vs 0.450 ms per round of both)
   if (mode == GS_BFS_AUTO)
-    mode = (n <= 8192 && n_slots >= 64)                                      ? GS_BFS_WORKGROUP
-           : (mv_ok && (n_slots >= 4 || (n_slots >= 2 && e->mv.XT > 256))) ? GS_BFS_MULTI
+    mode = (n <= 8192 && n_slots >= 64) ? GS_BFS_WORKGROUP
+           : mv_ok                      ? GS_BFS_MULTI
            : bin_ok                     ? GS_BFS_BINNED
                                         : GS_BFS_LEVEL;
   if (mode == GS_BFS_BINNED && !bin_ok) {

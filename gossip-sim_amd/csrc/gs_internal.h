@@ -212,6 +212,7 @@ struct Engine {
   // profiling
   struct Timed { std::vector<std::pair<hipEvent_t, hipEvent_t>> ev; double ms = 0; uint64_t n = 0; };
   std::map<std::string, Timed> timers;
+  std::string prof_only;  // ",fam1,fam2,": time only these families (GS_PROFILE_ONLY at create); empty: all
   std::vector<hipEvent_t> ev_pool;  // recycled events: no hipEventCreate per launch
   hipEvent_t ev_take();
   void tbegin(const char* fam, hipEvent_t* a);

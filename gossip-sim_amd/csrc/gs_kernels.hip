@@ -183,6 +183,63 @@ __global__ __launch_bounds__(1024) void k_rotate_decide(uint32_t N, uint64_t see
 // One thread per (rotating node, entry k). On a full entry the reference's loop
 // appends the first drawn peer that is not present, draws once more and breaks,
 // then drops the oldest: the ring's head slot is overwritten.
+// (rotating node rot_list[gid / NB], entry gid % NB): PushActiveSetEntry::rotate.
+template <int ASZP>
+__device__ inline void rotate_entry(const uint8_t* __restrict__ bucket, const uint64_t* __restrict__ P,
+                                    const uint32_t* __restrict__ IX, uint32_t* __restrict__ peers,
+                                    uint16_t* __restrict__ hl, const uint32_t* __restrict__ rot_list,
+                                    uint32_t* __restrict__ rot_changed, uint32_t N, uint32_t size, uint64_t seed,
+                                    uint32_t round, uint32_t gid) {
+    const uint32_t i = gid / NB, k = gid % NB;
+  const uint32_t u = rot_list[i];
+  const uint32_t ent = u * NB + k;
+  const uint16_t hv = hl[ent];
+  uint32_t head = hv & 0xFF, L = hv >> 8;
+  const uint32_t S = size;
+  uint32_t* row = peers + (size_t)ent * ASZP;
+  const uint64_t* Pk = P + (size_t)k * (N + 1);
+  const uint32_t LX = ix_log(N);
+  const uint32_t* IXk = IX + (size_t)k * ix_count(N);
+  constexpr int R = ASZP + 2;
+  uint32_t rem[R];
+  uint64_t remw[R];
+  int nr = 0;
+  const uint64_t wself = weight(k, bucket[u]);
+  rem_insert(rem, remw, nr, u, wself);
+  const uint64_t total = Pk[N];
+  uint64_t left = total - wself;
+  Philox s(seed, P_ROTATE, u, (round << 5) | k);
+  uint32_t changed = 0;
+  for (uint32_t drawn = 0; drawn + 1 < N; ++drawn) {
+    const uint64_t v = sample_below(left, s);
+    const uint32_t c = shuffle_pick(Pk, IXk, LX, total, v, rem, remw, nr);
+    const uint64_t wc = weight(k, bucket[c]);
+    left -= wc;
+    if (nr < R) rem_insert(rem, remw, nr, c, wc);
+    bool present = false;
+    for (uint32_t j = 0; j < L; ++j) {
+      uint32_t slot = head + j;
+      if (slot >= S) slot -= S;
+      present |= row[slot] == c;
+    }
+    if (present) continue;
+    if (L < S) {
+      uint32_t slot = head + L;
+      if (slot >= S) slot -= S;
+      row[slot] = c;
+      ++L;
+      changed |= 1u << slot;
+      continue;
+    }
+    row[head] = c;
+    changed |= 1u << head;
+    head = head + 1 == S ? 0 : head + 1;
+    break;
+  }
+  hl[ent] = (uint16_t)((L << 8) | head);
+  rot_changed[ent] = changed;
+}
+
 template <int ASZP>
 __global__ __launch_bounds__(256) void k_rotate_entries(const uint8_t* __restrict__ bucket,
                                                        const uint64_t* __restrict__ P, const uint32_t* __restrict__ IX,
@@ -192,56 +249,38 @@ __global__ __launch_bounds__(256) void k_rotate_entries(const uint8_t* __restric
                                                        uint32_t* __restrict__ rot_changed, uint32_t N, uint32_t size,
                                                        uint64_t seed, uint32_t round) {
   const uint32_t total = *rot_count * NB;
-  for (uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x; gid < total; gid += gridDim.x * blockDim.x) {
-    const uint32_t i = gid / NB, k = gid % NB;
-    const uint32_t u = rot_list[i];
-    const uint32_t ent = u * NB + k;
-    const uint16_t hv = hl[ent];
-    uint32_t head = hv & 0xFF, L = hv >> 8;
-    const uint32_t S = size;
-    uint32_t* row = peers + (size_t)ent * ASZP;
-    const uint64_t* Pk = P + (size_t)k * (N + 1);
-    const uint32_t LX = ix_log(N);
-    const uint32_t* IXk = IX + (size_t)k * ix_count(N);
-    constexpr int R = ASZP + 2;
-    uint32_t rem[R];
-    uint64_t remw[R];
-    int nr = 0;
-    const uint64_t wself = weight(k, bucket[u]);
-    rem_insert(rem, remw, nr, u, wself);
-    const uint64_t total = Pk[N];
-    uint64_t left = total - wself;
-    Philox s(seed, P_ROTATE, u, (round << 5) | k);
-    uint32_t changed = 0;
-    for (uint32_t drawn = 0; drawn + 1 < N; ++drawn) {
-      const uint64_t v = sample_below(left, s);
-      const uint32_t c = shuffle_pick(Pk, IXk, LX, total, v, rem, remw, nr);
-      const uint64_t wc = weight(k, bucket[c]);
-      left -= wc;
-      if (nr < R) rem_insert(rem, remw, nr, c, wc);
-      bool present = false;
-      for (uint32_t j = 0; j < L; ++j) {
-        uint32_t slot = head + j;
-        if (slot >= S) slot -= S;
-        present |= row[slot] == c;
-      }
-      if (present) continue;
-      if (L < S) {
-        uint32_t slot = head + L;
-        if (slot >= S) slot -= S;
-        row[slot] = c;
-        ++L;
-        changed |= 1u << slot;
-        continue;
-      }
-      row[head] = c;
-      changed |= 1u << head;
-      head = head + 1 == S ? 0 : head + 1;
-      break;
-    }
-    hl[ent] = (uint16_t)((L << 8) | head);
-    rot_changed[ent] = changed;
+  for (uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x; gid < total; gid += gridDim.x * blockDim.x)
+    rotate_entry<ASZP>(bucket, P, IX, peers, hl, rot_list, rot_changed, N, size, seed, round, gid);
+}
+
+// Small clusters (N <= RS_MAX): decide and rotate in ONE workgroup, one launch instead of two
+// (a dependent launch costs several us against ~5 us of work at C2's 3,000 nodes).
+constexpr uint32_t RS_MAX = 16384;
+template <int ASZP>
+__global__ __launch_bounds__(1024) void k_rotate_small(const uint8_t* __restrict__ bucket,
+                                                      const uint64_t* __restrict__ P, const uint32_t* __restrict__ IX,
+                                                      uint32_t* __restrict__ peers, uint16_t* __restrict__ hl,
+                                                      uint32_t* __restrict__ rot_list, uint32_t* __restrict__ rot_count,
+                                                      uint32_t* __restrict__ rot_count_other,
+                                                      uint32_t* __restrict__ rot_changed, uint32_t N, uint32_t size,
+                                                      uint64_t seed, uint32_t round, double p) {
+  __shared__ uint32_t lcount, base0;
+  if (threadIdx.x == 0) {
+    *rot_count_other = 0;  // the next rotation's counter
+    lcount = 0;
+    base0 = *rot_count;    // (zero unless a repeated round index appends)
   }
+  __syncthreads();
+  for (uint32_t u = threadIdx.x; u < N; u += blockDim.x) {  // DECIDE (gossip.rs:739-754), order-free
+    Philox s(seed, P_DECIDE, u, round);
+    if (unit_f64(s.next()) < p) rot_list[base0 + atomicAdd(&lcount, 1u)] = u;
+  }
+  __syncthreads();
+  const uint32_t n = base0 + lcount;
+  if (threadIdx.x == 0) *rot_count = n;
+  __threadfence_block();  // (this workgroup's rot_list stores before its entries read them)
+  for (uint32_t gid = threadIdx.x; gid < n * NB; gid += blockDim.x)
+    rotate_entry<ASZP>(bucket, P, IX, peers, hl, rot_list, rot_changed, N, size, seed, round, gid);
 }
 
 // A replaced peer gets a fresh filter: clear its ring slot's prune bit for every
@@ -273,11 +312,18 @@ hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear) {
     hipError_t r = hipMemsetAsync(cnt, 0, sizeof(uint32_t), e.st);
     if (r != hipSuccess) return r;
   }
-  hipLaunchKernelGGL(k_rotate_decide, dim3(grid_for(e.N, 4096, 256)), dim3(1024), 0, e.st, e.N, e.prm.seed, round,
-                     e.prm.rotation_probability, e.rot_list, cnt, e.rot_count + (par ^ 1u));
-  GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_rotate_entries<A>, dim3(grid_for((size_t)e.N * NB, 256, 2048)),
-                                              dim3(256), 0, e.st, e.bucket, e.P, e.IX, e.peers, e.hl, e.rot_list, cnt,
-                                              e.rot_changed, e.N, e.ASZ, e.prm.seed, round));
+  if (e.N <= RS_MAX) {
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_rotate_small<A>, dim3(1), dim3(1024), 0, e.st, e.bucket, e.P, e.IX,
+                                                e.peers, e.hl, e.rot_list, cnt, e.rot_count + (par ^ 1u),
+                                                e.rot_changed, e.N, e.ASZ, e.prm.seed, round,
+                                                e.prm.rotation_probability));
+  } else {
+    hipLaunchKernelGGL(k_rotate_decide, dim3(grid_for(e.N, 4096, 256)), dim3(1024), 0, e.st, e.N, e.prm.seed, round,
+                       e.prm.rotation_probability, e.rot_list, cnt, e.rot_count + (par ^ 1u));
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_rotate_entries<A>, dim3(grid_for((size_t)e.N * NB, 256, 2048)),
+                                                dim3(256), 0, e.st, e.bucket, e.P, e.IX, e.peers, e.hl, e.rot_list,
+                                                cnt, e.rot_changed, e.N, e.ASZ, e.prm.seed, round));
+  }
   hipError_t ro = launch_own_rows(e, e.rot_list, cnt);
   if (ro != hipSuccess) return ro;
   e.rot_parity = par;

@@ -53,8 +53,8 @@ enum { GS_NUM_BUCKETS = 25, GS_MAX_ACTIVE_SET_SIZE = 32, GS_MAX_NODES = (1 << 24
  * bin); MULTI = batched multi-source frontier BFS (a frontier entry is a node and
  * the mask of slots reaching it at that level: one row expansion and one record
  * per pushed-to peer serve every such slot; large clusters). AUTO picks
- * WORKGROUP (n <= 8,192 and >= 64 slots), else MULTI (>= 4 slots, or >= 2 slots
- * on graphs of >= 512 coarse bins: ~4M nodes and up), else BINNED, else LEVEL.
+ * WORKGROUP (n <= 8,192 and >= 64 slots), else MULTI (when its bin geometry fits LDS
+ * and its level area stays below 2^32 records), else BINNED, else LEVEL.
  * HYBRID = direction-optimizing multi-source BFS over the round's push graph: every node's
  * pushes for every slot built once per round as in-records grouped by destination, then
  * levels carrying only slot masks and distances -- top-down (frontier entries, atomicOr on
