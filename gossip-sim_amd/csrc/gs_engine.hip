@@ -1457,6 +1457,8 @@ int gs_part_xbfs_end(gs_engine* eh, int record) {
   PARTX(eh);
   if (e->x_group == 0xFFFFFFFFu) return fail(GS_ESTATE, "gs_part_xbfs_end: no group begun");
   e->tend("bfs", e->x_t0);
+  if (!e->mv_fused)
+    if (int s = ensure_inb(e)) return s;  // the gather's inbound rows (allocated on first use)
   hipEvent_t t0;
   e->tbegin("gather_consume", &t0);
   HIPC(mvx_gather_consume(*e, e->x_group, record != 0));
@@ -1474,7 +1476,9 @@ int gs_part_xround_finish(gs_engine* eh, uint32_t round, int record, uint32_t* n
   hipEvent_t t0;
   e->tbegin("consume", &t0);
   hipError_t r = hipMemsetAsync(e->slot_prunes, 0, e->S * 4, e->st);
-  if (r == hipSuccess) r = launch_consume_prune_g(*e, rec, false);  // send_prunes of own pruners (consumed at xbfs_end)
+  // consume_messages of every group's gathered rows (unless fused into xbfs_end), then
+  // send_prunes of own pruners
+  if (r == hipSuccess) r = launch_consume_prune_g(*e, rec, !e->mv_fused);
   if (r == hipSuccess) r = launch_part_emit(*e);                   // ... as records for the other ranks
   e->tend("consume", t0);
   HIPC(r);

@@ -23,6 +23,7 @@ Results on owned nodes, and every summary, are bit-identical to one engine over 
 nodes (tests/test_partition.py).
 """
 import ctypes as C
+import time
 
 import numpy as np
 
@@ -57,7 +58,8 @@ def partition_ranges(n, world, frontier=False):
 
 
 class PartitionedEngine:
-    def __init__(self, stakes, n_slots, *, group=None, device=0, exchange="auto", bfs="replicated", **engine_kw):
+    def __init__(self, stakes, n_slots, *, group=None, device=0, exchange="auto", bfs="replicated",
+                 profile=False, serialize=False, **engine_kw):
         import torch
         import torch.distributed as tdist
         self.torch, self.tdist, self.group = torch, tdist, group
@@ -99,6 +101,12 @@ class PartitionedEngine:
         self.records = 0       # prune records of the last round (all ranks)
         self.last_mode = None  # "records" / "dense" / None (no prunes)
         self.bytes_in = 0      # exchange bytes this rank received over all rounds (collective payload)
+        # profile=True: seconds per phase of this rank (device-synchronised wall time around
+        # each engine call; "exchange" = the collectives). serialize=True runs the ranks' engine
+        # calls one rank at a time (barriers in between), so ranks sharing one GPU time their
+        # own kernels alone: the per-rank share of a K-GPU run, measured on one device.
+        self.prof = {} if profile else None
+        self.serialize = serialize
 
     # the Engine's other calls (set_slots, init_active_sets, fail_nodes, readbacks) are
     # replicated or rank-local and need no exchange
@@ -127,6 +135,35 @@ class PartitionedEngine:
         self.dense = buf
         return buf
 
+    def _timed(self, name, fn):
+        """fn() on this rank, timed into prof[name] when profiling (one rank at a time when
+        serialize)."""
+        if self.prof is None:
+            return fn()
+        out = None
+        for r in range(self.world if self.serialize else 1):
+            if self.serialize:
+                self.tdist.barrier(group=self.group)
+            if not self.serialize or r == self.rank:
+                self.eng.sync()
+                t0 = time.perf_counter()
+                out = fn()
+                self.eng.sync()
+                self.prof[name] = self.prof.get(name, 0.0) + time.perf_counter() - t0
+        if self.serialize:
+            self.tdist.barrier(group=self.group)
+        return out
+
+    def _xchg(self, fn):
+        """A collective step, timed into prof["exchange"] when profiling."""
+        if self.prof is None:
+            return fn()
+        t0 = time.perf_counter()
+        out = fn()
+        self._done()
+        self.prof["exchange"] = self.prof.get("exchange", 0.0) + time.perf_counter() - t0
+        return out
+
     def _done(self):
         # the engine reads the buffers on its own stream: torch's collective must be complete
         if self.on_device:
@@ -146,30 +183,31 @@ class PartitionedEngine:
         wto = np.zeros(K, dtype=np.uint64)
         wfrom = np.zeros(K, dtype=np.uint64)
         levels = 0
+        T, X = self._timed, self._xchg
         for g in range(ng.value):
-            _check(L.gs_part_xbfs_begin(h, g, C.byref(n)))
+            T("begin", lambda: _check(L.gs_part_xbfs_begin(h, g, C.byref(n))))
             tot = torch.tensor([n.value], dtype=torch.int64, device=self.dev)
-            tdist.all_reduce(tot, group=self.group)
+            X(lambda: tdist.all_reduce(tot, group=self.group))
             d = 0
             while int(tot.item()) > 0:
-                _check(L.gs_part_xbfs_expand(h, d, wto.ctypes.data_as(C.c_void_p)))
+                T("expand", lambda: _check(L.gs_part_xbfs_expand(h, d, wto.ctypes.data_as(C.c_void_p))))
                 cto = torch.tensor(wto.astype(np.int64), device=self.dev)
                 cfrom = torch.zeros(K, dtype=torch.int64, device=self.dev)
-                tdist.all_to_all_single(cfrom, cto, group=self.group)
+                X(lambda: tdist.all_to_all_single(cfrom, cto, group=self.group))
                 wfrom[:] = cfrom.cpu().numpy().astype(np.uint64)
                 send = torch.empty(int(wto.sum()), dtype=torch.int64, device=self.dev)
-                _check(L.gs_part_xbfs_send(h, self._ptr(send), dev))
+                T("send", lambda: _check(L.gs_part_xbfs_send(h, self._ptr(send), dev)))
                 recv = torch.empty(int(wfrom.sum()), dtype=torch.int64, device=self.dev)
-                tdist.all_to_all_single(recv, send, output_split_sizes=[int(x) for x in wfrom],
-                                        input_split_sizes=[int(x) for x in wto], group=self.group)
+                X(lambda: tdist.all_to_all_single(recv, send, output_split_sizes=[int(x) for x in wfrom],
+                                                  input_split_sizes=[int(x) for x in wto], group=self.group))
                 self._done()
-                _check(L.gs_part_xbfs_apply(h, d, self._ptr(recv), wfrom.ctypes.data_as(C.c_void_p), dev,
-                                            C.byref(n)))
+                T("apply", lambda: _check(L.gs_part_xbfs_apply(h, d, self._ptr(recv), wfrom.ctypes.data_as(C.c_void_p),
+                                                               dev, C.byref(n))))
                 self.level_bytes += 8 * int(wfrom.sum())
                 tot = torch.tensor([n.value], dtype=torch.int64, device=self.dev)
-                tdist.all_reduce(tot, group=self.group)
+                X(lambda: tdist.all_reduce(tot, group=self.group))
                 d += 1
-            _check(L.gs_part_xbfs_end(h, int(bool(record))))
+            T("gather_consume", lambda: _check(L.gs_part_xbfs_end(h, int(bool(record)))))
             levels = max(levels, d)
         self.levels = levels
 
@@ -177,11 +215,12 @@ class PartitionedEngine:
         """One iteration of gossip_main.rs:449-564 over the partition."""
         torch, tdist, L, h, dev = self.torch, self.tdist, lib(), self.eng.h, int(self.on_device)
         n = C.c_uint32()
+        T = self._timed
         if self.frontier:
             self._frontier_bfs(record)
-            _check(L.gs_part_xround_finish(h, round_index, int(bool(record)), C.byref(n)))
+            T("prune", lambda: _check(L.gs_part_xround_finish(h, round_index, int(bool(record)), C.byref(n))))
         else:
-            _check(L.gs_part_round(h, round_index, int(bool(record)), C.byref(n)))
+            T("round", lambda: _check(L.gs_part_round(h, round_index, int(bool(record)), C.byref(n))))
         counts = [torch.zeros(1, dtype=torch.int64, device=self.dev) for _ in range(self.world)]
         tdist.all_gather(counts, torch.tensor([n.value], dtype=torch.int64, device=self.dev), group=self.group)
         counts = [int(c.item()) for c in counts]
@@ -198,30 +237,30 @@ class PartitionedEngine:
                                    "use exchange='auto' or 'dense'")
             if dense:
                 self._dense_buffer()
-                _check(L.gs_part_prunes_dense_out(h, self._ptr(self.dense), dev))
-                tdist.all_reduce(self.dense, group=self.group)
+                T("prunes_out", lambda: _check(L.gs_part_prunes_dense_out(h, self._ptr(self.dense), dev)))
+                self._xchg(lambda: tdist.all_reduce(self.dense, group=self.group))
                 self._done()
-                _check(L.gs_part_prunes_dense_in(h, self._ptr(self.dense), dev))
+                T("prunes_in", lambda: _check(L.gs_part_prunes_dense_in(h, self._ptr(self.dense), dev)))
                 self.bytes_in += dense_bytes
                 self.last_mode = "dense"
             else:
                 mine = torch.zeros(2 * m, dtype=torch.int32, device=self.dev)
                 if n.value:
-                    _check(L.gs_part_prunes_out(h, self._ptr(mine), dev))
+                    T("prunes_out", lambda: _check(L.gs_part_prunes_out(h, self._ptr(mine), dev)))
                 parts = [torch.zeros(2 * m, dtype=torch.int32, device=self.dev) for _ in range(self.world)]
-                tdist.all_gather(parts, mine, group=self.group)
+                self._xchg(lambda: tdist.all_gather(parts, mine, group=self.group))
                 recs = torch.cat([p[:2 * c] for p, c in zip(parts, counts)])
                 self._done()
-                _check(L.gs_part_prunes_in(h, self._ptr(recs), sum(counts), dev))
+                T("prunes_in", lambda: _check(L.gs_part_prunes_in(h, self._ptr(recs), sum(counts), dev)))
                 self.bytes_in += rec_bytes
                 self.last_mode = "records"
         self.records = sum(counts)
-        self.eng.chance_to_rotate(round_index)
+        T("rotate", lambda: self.eng.chance_to_rotate(round_index))
         if record:
-            _check(L.gs_part_stats_out(h, self._ptr(self.stats), dev))
-            tdist.all_reduce(self.stats, group=self.group)
+            T("stats", lambda: _check(L.gs_part_stats_out(h, self._ptr(self.stats), dev)))
+            self._xchg(lambda: tdist.all_reduce(self.stats, group=self.group))
             self._done()
-            _check(L.gs_part_stats_in(h, self._ptr(self.stats), dev))
+            T("stats_in", lambda: _check(L.gs_part_stats_in(h, self._ptr(self.stats), dev)))
 
     def owned(self, arr):
         """The owned slice of a per-node array."""

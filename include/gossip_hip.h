@@ -253,8 +253,9 @@ int gs_part_prunes_dense_in(gs_engine* e, const void* src, int src_device);
  *     ALL-TO-ALL the K counts, then gs_part_xbfs_send(buf) -> ALL-TO-ALL (split by words_to /
  *       words_from, u64 words: per message the owner's bin counts, then the records)
  *     gs_part_xbfs_apply(d, recv, words_from[K], &n)  apply what every rank pushed here
- *   gs_part_xbfs_end(record)                         gather + consume_messages of the group's own nodes
- * then gs_part_xround_finish(round, record, &n_records) (send_prunes of own pruners)
+ *   gs_part_xbfs_end(record)                         gather of the group's own nodes (inbound rows)
+ * then gs_part_xround_finish(round, record, &n_records) (consume_messages of every group's rows,
+ * send_prunes of own pruners; with GS_MV_FUSED=1 the consume runs fused in xbfs_end instead)
  * in place of gs_part_round; the prune and statistics exchanges follow as above. */
 int gs_part_xbfs_groups(gs_engine* e, uint32_t* n_groups);
 int gs_part_xbfs_begin(gs_engine* e, uint32_t group, uint32_t* n_local);
