@@ -303,6 +303,29 @@ def c5_leg(gs, synth, args, nodes=10_000_000, slots=None, warmup=3, steps=10):
                                      "B_prop (SURVEY 8d), summed over slots", f"bfs_{mode}_c5")}
 
 
+class profile_only:
+    """GS_PROFILE_ONLY=<families> around engine creation: the engine records timing events
+    only around those families (each recorded family boundary idles the GPU several us;
+    the C3 leg's one-slot engines had ~34 us of such gaps per round)."""
+
+    def __init__(self, fams):
+        self.fams, self.old = fams, None
+
+    def __enter__(self):
+        self.old = os.environ.get("GS_PROFILE_ONLY")
+        os.environ["GS_PROFILE_ONLY"] = self.fams
+        return self
+
+    def __exit__(self, *exc):
+        if self.old is None:
+            os.environ.pop("GS_PROFILE_ONLY", None)
+        else:
+            os.environ["GS_PROFILE_ONLY"] = self.old
+
+
+BFS_FAMS = "bfs,gather,gather_consume"
+
+
 def c3_leg(gs, synth, args, nodes=100_000, warmup=5, steps=20):
     """BASELINE C3's share of one GPU: ASZ 12 and 20 (sims 0 and 8 of the 16-sim sweep
     dealt over 8 GPUs), one engine (one slot) per value, origin rank 1."""
@@ -311,8 +334,9 @@ def c3_leg(gs, synth, args, nodes=100_000, warmup=5, steps=20):
     origin = int(np.argmax(stakes))
     engs = []
     for asz in (12, 20):
-        e = gs.Engine(stakes, 1, fanout=args.fanout, active_set_size=asz, rotation_probability=0.013333,
-                      seed=args.seed, device=0, profile=True, bfs_mode=args.large_mode)
+        with profile_only(BFS_FAMS):  # (only the BFS families are reported)
+            e = gs.Engine(stakes, 1, fanout=args.fanout, active_set_size=asz, rotation_probability=0.013333,
+                          seed=args.seed, device=0, profile=True, bfs_mode=args.large_mode)
         e.set_slots([origin], args.min_ingress, args.threshold)
         e.init_active_sets()
         engs.append((asz, e))
@@ -391,9 +415,10 @@ def sweep_workload(gs, synth, args, rank, world, dev, barrier, reduce):
     E = 0.0
     eng = None
     if shard:
-        eng = gs.Engine(stakes, len(shard), fanout=args.fanout, active_set_size=args.active_set_size,
-                        rotation_probability=0.013333, seed=seed, device=dev, profile=True,
-                        bfs_mode=args.large_mode)
+        with profile_only(BFS_FAMS):  # (roofline_rank0 reads the BFS families only)
+            eng = gs.Engine(stakes, len(shard), fanout=args.fanout, active_set_size=args.active_set_size,
+                            rotation_probability=0.013333, seed=seed, device=dev, profile=True,
+                            bfs_mode=args.large_mode)
         eng.set_slots([org_all[i] for i in shard], args.min_ingress, [thr_all[i] for i in shard])
         eng.init_active_sets()
         if any(fr_all[i] for i in shard):
@@ -454,7 +479,7 @@ def c3_sweep_workload(gs, synth, args, rank, world, dev, barrier, reduce):
     engs = []
     for asz in mine:
         e = gs.Engine(stakes, 1, fanout=args.fanout, active_set_size=asz, rotation_probability=0.013333, seed=seed,
-                      device=dev, profile=True, bfs_mode=args.large_mode)
+                      device=dev, profile=False, bfs_mode=args.large_mode)  # (no kernel times reported)
         e.set_slots([origin], args.min_ingress, args.threshold)
         e.init_active_sets()
         engs.append((asz, e))

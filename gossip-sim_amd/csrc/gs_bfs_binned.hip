@@ -777,24 +777,8 @@ __global__ void k_own_rows(const uint8_t* __restrict__ bucket, const uint32_t* _
                            const uint32_t* __restrict__ count, uint32_t n_all, uint32_t ORW,
                            const uint8_t* __restrict__ fcls, uint32_t* __restrict__ own) {
   const uint32_t n = count ? *count : n_all;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t u = list ? list[i] : i;
-    const uint32_t b = bucket[u];
-    const uint32_t ent = u * NB + b;
-    uint32_t row[ASZP];
-    load_row<ASZP>(peers + (size_t)ent * ASZP, row);
-    uint32_t* dst = own + (size_t)u * ORW;
-    uint4* d4 = reinterpret_cast<uint4*>(dst);
-#pragma unroll
-    for (int q = 0; q < ASZP / 4; ++q) d4[q] = make_uint4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
-    dst[ASZP] = (uint32_t)hl[ent] | (b << 16);
-    if (fcls) {
-#pragma unroll
-      for (int q = 0; q < ASZP / 4; ++q)
-        dst[ASZP + 1 + q] = (uint32_t)fcls[row[4 * q]] | ((uint32_t)fcls[row[4 * q + 1]] << 8) |
-                            ((uint32_t)fcls[row[4 * q + 2]] << 16) | ((uint32_t)fcls[row[4 * q + 3]] << 24);
-    }
-  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    own_row<ASZP>(bucket, peers, hl, ORW, fcls, own, list ? list[i] : i);
 }
 
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count) {

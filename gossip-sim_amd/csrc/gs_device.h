@@ -176,6 +176,31 @@ __device__ inline void load_row(const uint32_t* __restrict__ src, uint32_t (&row
   }
 }
 
+// Own-bucket entry row of node u (the entry it uses for every origin whose bucket is at
+// least its own, push_active_set.rs:38-52): own[u] = peers[u][bucket[u]] and, in word
+// ASZP, hl | bucket << 16; with fcls (the multi-source BFS) words ASZP + 1 .. hold the
+// peers' failure classes, one byte each, so a row and its failure test are one line.
+template <int ASZP>
+__device__ inline void own_row(const uint8_t* __restrict__ bucket, const uint32_t* __restrict__ peers,
+                               const uint16_t* __restrict__ hl, uint32_t ORW, const uint8_t* __restrict__ fcls,
+                               uint32_t* __restrict__ own, uint32_t u) {
+  const uint32_t b = bucket[u];
+  const uint32_t ent = u * NB + b;
+  uint32_t row[ASZP];
+  load_row<ASZP>(peers + (size_t)ent * ASZP, row);
+  uint32_t* dst = own + (size_t)u * ORW;
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+  for (int q = 0; q < ASZP / 4; ++q) d4[q] = make_uint4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+  dst[ASZP] = (uint32_t)hl[ent] | (b << 16);
+  if (fcls) {
+#pragma unroll
+    for (int q = 0; q < ASZP / 4; ++q)
+      dst[ASZP + 1 + q] = (uint32_t)fcls[row[4 * q]] | ((uint32_t)fcls[row[4 * q + 1]] << 8) |
+                          ((uint32_t)fcls[row[4 * q + 2]] << 16) | ((uint32_t)fcls[row[4 * q + 3]] << 24);
+  }
+}
+
 // PushActiveSet::get_nodes(..).take(fanout) (gossip.rs:527-536, push_active_set.rs:128-141):
 // the first `fanout` peers in FIFO order whose filter lacks the origin -- i.e.
 // not pruned for this slot and not the origin itself. Returns physical ring slots.

@@ -9,6 +9,8 @@
 //   k_consume_prune    consume_messages + ReceivedCache::record/prune + send_prunes +
 //                      prune_connections (gossip.rs:618-737, received_cache.rs:27-131)
 //   k_stats_*          the measured-round statistics inserts (gossip_main.rs:480-563)
+#include <cstdlib>
+
 #include <hipcub/hipcub.hpp>
 
 #include "gs_device.h"
@@ -283,6 +285,46 @@ __global__ __launch_bounds__(1024) void k_rotate_small(const uint8_t* __restrict
     rotate_entry<ASZP>(bucket, P, IX, peers, hl, rot_list, rot_changed, N, size, seed, round, gid);
 }
 
+// Larger clusters: decide, rotate and refresh the own rows in ONE launch instead of three
+// (k_rotate_decide, k_rotate_entries, k_own_rows: ~12 us of dependent launches per round at
+// C3's 100k nodes). Each 256-thread block takes RF_NODES consecutive nodes (two per
+// thread), lists its rotating nodes in LDS, appends them to rot_list with one atomic,
+// rotates their entries (one (node, entry) per thread: p x NB ~ 0.33 entries per node, so
+// ~170 per block) and then rewrites their own rows -- everything a block touches is its own
+// nodes' rows, so no grid-wide ordering is needed.
+constexpr uint32_t RF_THREADS = 256;
+constexpr uint32_t RF_NODES = 512;
+template <int ASZP>
+__global__ __launch_bounds__(RF_THREADS) void k_rotate_fused(const uint8_t* __restrict__ bucket,
+                                                            const uint64_t* __restrict__ P, const uint32_t* __restrict__ IX,
+                                                            uint32_t* __restrict__ peers, uint16_t* __restrict__ hl,
+                                                            uint32_t* __restrict__ rot_list, uint32_t* __restrict__ rot_count,
+                                                            uint32_t* __restrict__ rot_count_other,
+                                                            uint32_t* __restrict__ rot_changed, uint32_t N, uint32_t size,
+                                                            uint64_t seed, uint32_t round, double p, uint32_t ORW,
+                                                            const uint8_t* __restrict__ fcls, uint32_t* __restrict__ own) {
+  __shared__ uint32_t lids[RF_NODES], lcount, lbase;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *rot_count_other = 0;  // the next rotation's counter
+  if (threadIdx.x == 0) lcount = 0;
+  __syncthreads();
+  const uint32_t lo = blockIdx.x * RF_NODES, hi = min(N, lo + RF_NODES);
+  for (uint32_t u = lo + threadIdx.x; u < hi; u += RF_THREADS) {  // DECIDE (gossip.rs:739-754), order-free
+    Philox s(seed, P_DECIDE, u, round);
+    if (unit_f64(s.next()) < p) lids[atomicAdd(&lcount, 1u)] = u;
+  }
+  __syncthreads();
+  const uint32_t n = lcount;
+  if (n == 0) return;  // (block-uniform)
+  if (threadIdx.x == 0) lbase = atomicAdd(rot_count, n);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += RF_THREADS) rot_list[lbase + i] = lids[i];
+  for (uint32_t gid = threadIdx.x; gid < n * NB; gid += RF_THREADS)  // (rotate_entry reads the LDS list)
+    rotate_entry<ASZP>(bucket, P, IX, peers, hl, lids, rot_changed, N, size, seed, round, gid);
+  if (!own) return;
+  __syncthreads();  // (the block's entry rows and ring heads are written before its own rows read them)
+  for (uint32_t i = threadIdx.x; i < n; i += RF_THREADS) own_row<ASZP>(bucket, peers, hl, ORW, fcls, own, lids[i]);
+}
+
 // A replaced peer gets a fresh filter: clear its ring slot's prune bit for every
 // slot whose origin uses that entry.
 __global__ void k_rotate_clear(size_t mso, size_t msu, uint32_t S, const uint8_t* __restrict__ bucket,
@@ -306,6 +348,8 @@ hipError_t launch_rotate_clear(Engine& e) {
 }
 
 hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear) {
+  // GS_ROT_SPLIT=1: the three-launch rotation (decide, entries, own rows) for N > RS_MAX
+  static const bool rot_split = std::getenv("GS_ROT_SPLIT") && std::getenv("GS_ROT_SPLIT")[0] == '1';
   const uint32_t par = round & 1u;
   uint32_t* cnt = e.rot_count + par;
   if (e.rot_have_prev && par == e.rot_parity) {  // rounds not consecutive: this counter was not pre-zeroed
@@ -317,6 +361,12 @@ hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear) {
                                                 e.peers, e.hl, e.rot_list, cnt, e.rot_count + (par ^ 1u),
                                                 e.rot_changed, e.N, e.ASZ, e.prm.seed, round,
                                                 e.prm.rotation_probability));
+  } else if (!rot_split) {
+    const uint32_t grid = (e.N + RF_NODES - 1) / RF_NODES;
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_rotate_fused<A>, dim3(grid), dim3(RF_THREADS), 0, e.st, e.bucket,
+                                                e.P, e.IX, e.peers, e.hl, e.rot_list, cnt, e.rot_count + (par ^ 1u),
+                                                e.rot_changed, e.N, e.ASZ, e.prm.seed, round,
+                                                e.prm.rotation_probability, e.ORW, e.mv_fcls, e.own));
   } else {
     hipLaunchKernelGGL(k_rotate_decide, dim3(grid_for(e.N, 4096, 256)), dim3(1024), 0, e.st, e.N, e.prm.seed, round,
                        e.prm.rotation_probability, e.rot_list, cnt, e.rot_count + (par ^ 1u));
@@ -324,8 +374,10 @@ hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear) {
                                                 dim3(256), 0, e.st, e.bucket, e.P, e.IX, e.peers, e.hl, e.rot_list,
                                                 cnt, e.rot_changed, e.N, e.ASZ, e.prm.seed, round));
   }
-  hipError_t ro = launch_own_rows(e, e.rot_list, cnt);
-  if (ro != hipSuccess) return ro;
+  if (e.N <= RS_MAX || rot_split) {  // (the fused kernel refreshed its nodes' own rows itself)
+    hipError_t ro = launch_own_rows(e, e.rot_list, cnt);
+    if (ro != hipSuccess) return ro;
+  }
   e.rot_parity = par;
   e.rot_have_prev = true;
   e.rot_clear_pending = true;
