@@ -863,6 +863,8 @@ __global__ __launch_bounds__(MV_GT) void k_mv_gather(MvArgs a) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, BP = 1u << a.BSF, Sg = a.Sg, v0 = (a.flo + f) << a.BSF;
   if (v0 >= a.vhi) return;
   const uint32_t nv = min(BP, a.vhi - v0), gcap = a.gcap;
+  if (a.clear_vis)  // (the BFS is over and the gather does not read vis)
+    for (uint32_t i = tid; i < nv; i += MV_GT) a.vis[v0 + i] = 0;
   const MvCsr L = mv_csr_lds(smem, BP, gcap);
   bool over = false;
   mv_bin_csr(a, f, nv, gcap, L, [&](uint32_t lo, uint32_t hi, uint32_t base) {
@@ -980,6 +982,8 @@ __global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void
   const uint32_t tid = threadIdx.x, lane = tid & 63, BP = 1u << a.BSF, Sg = a.Sg, v0 = (a.flo + f) << a.BSF;
   if (v0 >= a.vhi) return;
   const uint32_t nv = min(BP, a.vhi - v0), gcap = a.gcap_c;
+  if (a.clear_vis)
+    for (uint32_t i = tid; i < nv; i += MV_GT) a.vis[v0 + i] = 0;
   uint32_t* wscr = reinterpret_cast<uint32_t*>(smem) + (tid >> 6) * MV_WSCR;  // [64] keys, [CACHE_CAP] cache
   const MvCsr L = mv_csr_lds(smem + MV_CSCR, BP, gcap);
   const size_t PAIRS = a.PAIRS;
@@ -1289,7 +1293,7 @@ MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.origin = e.origin; a.mask = e.mask; a.gt = e.mv_gtab + (size_t)g * GT_STRIDE;
   a.hops = e.hops; a.cnt = e.cnt; a.inb = e.inb; a.egress = e.egress; a.err = e.err;
   a.vis = e.mv_vis; a.lvl = e.lvl; a.hlvl = e.mv_hlvl_dev; a.T = e.mv_T; a.area = e.mv_area; a.ctr = e.mv_ctr;
-  a.dpair = e.mv_dpair; a.hprof = nullptr;
+  a.dpair = e.mv_dpair; a.hprof = nullptr; a.clear_vis = 0;
   a.pool = e.mv_pool; a.pused = e.mv_pused;
   a.N = e.N; a.SP = e.SP; a.ASZ = e.ASZ; a.fanout = e.fanout; a.capin = e.capin; a.s0 = gr.s0; a.Sg = gr.sg;
   a.UB = e.mv.UB; a.BSC = e.mv.BSC; a.BSF = e.mv.BSF; a.nbc = e.mv.nbc; a.nbf = e.mv.nbf; a.TW = e.mv.TW;
@@ -1525,7 +1529,8 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     }
     hipEvent_t t0;
     e.tbegin("bfs", &t0);
-    if ((r = hipMemsetAsync(e.mv_vis, 0, (size_t)e.N * 4, e.st))) return r;
+    if (!e.mv_vis_clean && (r = hipMemsetAsync(e.mv_vis, 0, (size_t)e.N * 4, e.st))) return r;
+    e.mv_vis_clean = false;
     uint32_t nlev = 254;  // (the gather reads the levels' sizes; empty levels end the BFS)
     const std::vector<uint32_t>& pv = e.mv_pred[g];
     if (pv.empty() || polled_only || e.mv_diag) {
@@ -1565,8 +1570,12 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     }
     e.tend("bfs", t0);
     e.tbegin(consume ? "gather_consume" : "gather", &t0);
+    // an unpartitioned engine's fine bins cover every node: the gather leaves vis zeroed
+    // for the next BFS (one memset launch less per group and round)
+    a.clear_vis = e.part_on ? 0u : 1u;
     if (consume) hipLaunchKernelGGL(k_mv_consume, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a);
     else hipLaunchKernelGGL(k_mv_gather, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a);
+    e.mv_vis_clean = a.clear_vis != 0;
     e.tend(consume ? "gather_consume" : "gather", t0);
     if (e.mv_diag) {  // GS_MV_DIAG=1: entries and records of the group's BFS (diagnostics)
       std::vector<uint32_t> pu(fno);

@@ -61,6 +61,7 @@ struct CgArgs {
                                     // GS_FLAG_NARROW_WAVE_PATH: (4, 4, 8), so small tests reach every path
   size_t PAIRS;
   int record;
+  int zero_sp;  // k_cg_consume zeroes slot_prunes (block 0) for the k_cg_prune that follows
 };
 
 // ---- consume, register path (1 <= c <= 16) ----
@@ -370,6 +371,8 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_consume(CgArgs a) {
   __shared__ uint32_t scr_all[CG_WAVES * CG_SCR];
   uint32_t* scr = scr_all + (threadIdx.x >> 6) * CG_SCR;
   uint32_t errf = 0;
+  if (a.zero_sp && blockIdx.x == 0)  // (instead of a memset launch before this kernel)
+    for (uint32_t i = threadIdx.x; i < a.S; i += CG_THREADS) a.slot_prunes[i] = 0;
   const uint32_t P = (uint32_t)a.PAIRS;
   for (uint32_t p0 = blockIdx.x * CG_THREADS; p0 < P; p0 += gridDim.x * CG_THREADS) {
     const uint32_t q = p0 + threadIdx.x;
@@ -471,7 +474,7 @@ __global__ __launch_bounds__(CG_THREADS) void k_cg_prune(CgArgs a) {
 }  // namespace
 
 // consume_messages + send_prunes + prune_connections of every slot (gs_round's step path).
-hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume) {
+hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume, bool zero_slot_prunes) {
   CgArgs a;
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.origin = e.origin; a.obkt = e.obkt;
   a.own = e.own; a.ORW = e.ORW;
@@ -484,10 +487,11 @@ hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume) {
   a.mso = e.mso;
   a.msu = e.msu;
   const bool narrow = (e.prm.flags & GS_FLAG_NARROW_WAVE_PATH) != 0;
+  a.zero_sp = consume && zero_slot_prunes ? 1 : 0;
   a.lane_c = narrow ? 4u : 16u;
   a.lane_l = narrow ? 4u : LANE_L;
   a.wave_c = narrow ? 8u : 64u;
-  // (slot_prunes was zeroed by launch_consume_prune)
+  // (slot_prunes was zeroed by the caller, or is by k_cg_consume when zero_slot_prunes)
   const uint32_t grid = (uint32_t)std::min<size_t>((e.PAIRS + CG_THREADS - 1) / CG_THREADS, 8192);
   if (consume) hipLaunchKernelGGL(k_cg_consume, dim3(grid), dim3(CG_THREADS), 0, e.st, a);
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_cg_prune<A>, dim3(grid), dim3(CG_THREADS), 0, e.st, a));

@@ -142,6 +142,7 @@ struct Engine {
   uint32_t bfs_level = 0;  // the level loop's current level (reported when a level wait times out)
   bool mv_diag = false;  // GS_MV_DIAG=1
   bool mv_line = false;   // multi: prune masks live in the row table's node lines (msu = 32)
+  bool mv_vis_clean = true;  // mv_vis is all zero (allocated zeroed; a clearing gather ran last)
   bool mv_fused = false;  // gs_round: gather, then k_cg_consume; GS_MV_FUSED=1: fused gather + consume (slower at C4)
   // direction-optimizing BFS over the round's push graph (GS_BFS_HYBRID, gs_bfs_hybrid.hip);
   // it shares the multi BFS's layout, groups, queues, T rows and record area
@@ -296,7 +297,7 @@ hipError_t mvx_gather_consume(Engine& e, uint32_t g, bool record);
 // own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
-hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume = true);
+hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume = true, bool zero_slot_prunes = false);
 // node-range partition (gs_partition.hip)
 size_t part_stats_words(const Engine& e);
 hipError_t launch_part_stats_pack(Engine& e);

@@ -849,8 +849,8 @@ hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply,
   a.mso = e.mso; a.msu = e.msu;
   const uint32_t grid = grid_for(e.PAIRS, 256, 8192);
   hipError_t r;
+  if (consume && prune && apply) return launch_consume_prune_g(e, record, true, true);  // gs_consume_g.hip
   if (prune && (r = hipMemsetAsync(e.slot_prunes, 0, e.S * 4, e.st)) != hipSuccess) return r;
-  if (consume && prune && apply) return launch_consume_prune_g(e, record);  // gs_consume_g.hip
 #define GS_CP(C, P, A) hipLaunchKernelGGL((k_consume_prune<C, P, A>), dim3(grid), dim3(256), 0, e.st, a)
   if (consume && !prune && !apply) GS_CP(true, false, false);
   else if (!consume && prune && !apply) GS_CP(false, true, false);

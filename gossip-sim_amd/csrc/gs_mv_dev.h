@@ -34,6 +34,7 @@ struct MvArgs {
   uint8_t* egress;        // node-major [NP][SP] (nodes [vlo, vhi))
   uint32_t* err;
   uint32_t* vis;          // [N] slot masks reached
+  uint32_t clear_vis;     // the gather zeroes its bins' vis words (the next BFS needs no memset)
   uint32_t* lvl;          // [256] frontier entries per level
   uint32_t* hlvl;         // host-mapped [256]: expand(d) writes lvl[d] here (the polled loop)
   uint32_t* dpair;        // [258] level of expand/apply pair i (predicted loop): head writes [0], apply(i) [i + 1]
