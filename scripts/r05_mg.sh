@@ -5,7 +5,7 @@
 # rendezvous, sharding and assembly; both ranks share one device, so not scaling.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/r05/mg
-P=profiles/r05/mg
+P=gpurun_out/r05/mg  # (copied into profiles/r05/mg/ after the call)
 mkdir -p $OUT $P
 GS_BENCH_DEVICE=0 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29543 bench.py --gpus 2 --steps 20 --warmup 5 --check-shard > $OUT/c2_w2.log 2>&1 || { tail -5 $OUT/c2_w2.log; exit 1; }
 grep '"metric"' $OUT/c2_w2.log | tail -1 > $P/c2_w2.json; cut -c1-300 $P/c2_w2.json; echo
