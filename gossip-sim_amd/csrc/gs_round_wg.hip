@@ -48,6 +48,9 @@ constexpr uint32_t CSR_NPT = (RWG_CSR_REG_NODES + RWG_THREADS - 1) / RWG_THREADS
 static_assert(CSR_NPT * RWG_THREADS >= RWG_CSR_REG_NODES, "register-staged CSR covers its node bound");
 constexpr uint32_t RWG_SCR = 128;  // per-wave LDS scratch (u32): staged cache keys / prune keys
 constexpr uint32_t LANE_C = 16;    // register path: in-degree <= 16
+#ifndef RWG_IN
+#define RWG_IN 4  // nodes per trip of the setup loop (C2: 3,000 nodes = 4 per thread)
+#endif
 constexpr int LANE_L = 16;         // register prune path: cache entry <= 16 keys (the wave path
                                    // takes longer entries; at prune time they are rare)
 
@@ -644,13 +647,32 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   unsigned long long t_mark = PROF && a.phase_clk && tid == 0 ? wall_clock64() : 0;
 
   for (uint32_t i = tid; i < (N + 1) / 2; i += RWG_THREADS) cntw[i] = 0;
-  for (uint32_t v = tid; v < N; v += RWG_THREADS) {
-    hops_l[v] = 0xFF;
-    pm_l[v] = 0;
-    mk_l[v] = (PMT)ntl(&a.mask[base + v]);
-    const uint32_t b = min((uint32_t)a.bucket[v], ob);  // entry the origin uses (push_active_set.rs:38-52)
-    const uint32_t hv = a.hl[v * NB + b];
-    nl_l[v] = (uint16_t)((hv & 0x1Fu) | ((hv >> 8) << 5) | (b << 11));
+  // Each node's mask word, bucket and ring head/len (of the entry the origin uses,
+  // push_active_set.rs:38-52), RWG_IN nodes per trip: the trip's bucket loads, then its
+  // hl loads, are issued together (one node per trip waited for two dependent round trips
+  // per node)
+  for (uint32_t v0 = tid; v0 < N; v0 += RWG_IN * RWG_THREADS) {
+    uint32_t bk[RWG_IN], mw[RWG_IN], hv[RWG_IN];
+#pragma unroll
+    for (uint32_t k = 0; k < RWG_IN; ++k) {
+      const uint32_t v = v0 + k * RWG_THREADS;
+      bk[k] = v < N ? min((uint32_t)a.bucket[v], ob) : 0u;
+      mw[k] = v < N ? ntl(&a.mask[base + v]) : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < RWG_IN; ++k) {
+      const uint32_t v = v0 + k * RWG_THREADS;
+      hv[k] = v < N ? a.hl[v * NB + bk[k]] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < RWG_IN; ++k) {
+      const uint32_t v = v0 + k * RWG_THREADS;
+      if (v >= N) break;
+      hops_l[v] = 0xFF;
+      pm_l[v] = 0;
+      mk_l[v] = (PMT)mw[k];
+      nl_l[v] = (uint16_t)((hv[k] & 0x1Fu) | ((hv[k] >> 8) << 5) | (bk[k] << 11));
+    }
   }
   for (uint32_t i = tid; i < 256; i += RWG_THREADS) hist[i] = 0;
   for (uint32_t i = tid; i < W; i += RWG_THREADS) bm_l[i] = 0;
