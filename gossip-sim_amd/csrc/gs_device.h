@@ -322,4 +322,65 @@ __device__ inline void sort_net(uint32_t (&r)[M]) {
 }
 __device__ inline void sort16(uint32_t (&r)[16]) { sort_net<16>(r); }
 
+// One thread per (rotating node, entry k). On a full entry the reference's loop
+// appends the first drawn peer that is not present, draws once more and breaks,
+// then drops the oldest: the ring's head slot is overwritten.
+// (rotating node rot_list[gid / NB], entry gid % NB): PushActiveSetEntry::rotate.
+template <int ASZP>
+__device__ inline void rotate_entry(const uint8_t* __restrict__ bucket, const uint64_t* __restrict__ P,
+                                    const uint32_t* __restrict__ IX, uint32_t* __restrict__ peers,
+                                    uint16_t* __restrict__ hl, const uint32_t* __restrict__ rot_list,
+                                    uint32_t* __restrict__ rot_changed, uint32_t N, uint32_t size, uint64_t seed,
+                                    uint32_t round, uint32_t gid) {
+    const uint32_t i = gid / NB, k = gid % NB;
+  const uint32_t u = rot_list[i];
+  const uint32_t ent = u * NB + k;
+  const uint16_t hv = hl[ent];
+  uint32_t head = hv & 0xFF, L = hv >> 8;
+  const uint32_t S = size;
+  uint32_t* row = peers + (size_t)ent * ASZP;
+  const uint64_t* Pk = P + (size_t)k * (N + 1);
+  const uint32_t LX = ix_log(N);
+  const uint32_t* IXk = IX + (size_t)k * ix_count(N);
+  constexpr int R = ASZP + 2;
+  uint32_t rem[R];
+  uint64_t remw[R];
+  int nr = 0;
+  const uint64_t wself = weight(k, bucket[u]);
+  rem_insert(rem, remw, nr, u, wself);
+  const uint64_t total = Pk[N];
+  uint64_t left = total - wself;
+  Philox s(seed, P_ROTATE, u, (round << 5) | k);
+  uint32_t changed = 0;
+  for (uint32_t drawn = 0; drawn + 1 < N; ++drawn) {
+    const uint64_t v = sample_below(left, s);
+    const uint32_t c = shuffle_pick(Pk, IXk, LX, total, v, rem, remw, nr);
+    const uint64_t wc = weight(k, bucket[c]);
+    left -= wc;
+    if (nr < R) rem_insert(rem, remw, nr, c, wc);
+    bool present = false;
+    for (uint32_t j = 0; j < L; ++j) {
+      uint32_t slot = head + j;
+      if (slot >= S) slot -= S;
+      present |= row[slot] == c;
+    }
+    if (present) continue;
+    if (L < S) {
+      uint32_t slot = head + L;
+      if (slot >= S) slot -= S;
+      row[slot] = c;
+      ++L;
+      changed |= 1u << slot;
+      continue;
+    }
+    row[head] = c;
+    changed |= 1u << head;
+    head = head + 1 == S ? 0 : head + 1;
+    break;
+  }
+  hl[ent] = (uint16_t)((L << 8) | head);
+  rot_changed[ent] = changed;
+}
+
+
 }  // namespace gs

@@ -346,6 +346,8 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   // one-kernel round (gs_round): per-slot state in LDS, at most 160 KiB per workgroup
   e->fused = mode == GS_BFS_WORKGROUP && !(prm->flags & GS_FLAG_SPLIT_ROUND) &&
              round_wg_lds_bytes(n, e->fcap, e->ASZP) <= 160 * 1024;
+  // rotation ahead of the fused round (one-workgroup rotation sizes; GS_ROT_AHEAD=0: off)
+  e->rot_ahead_ok = e->fused && n <= 16384 && !(std::getenv("GS_ROT_AHEAD") && std::getenv("GS_ROT_AHEAD")[0] == '0');
 
   const size_t N = n, S = n_slots, PAIRS = e->PAIRS, NP = e->NP;
   e->SP = (uint32_t)((S + 3) & ~(size_t)3);
@@ -664,6 +666,7 @@ int gs_set_active_set_entry(gs_engine* eh, uint32_t node, uint32_t bucket, const
   uint16_t hv = (uint16_t)(len << 8);
   HIPC(hipMemcpyAsync(e->peers + ent * e->ASZP, row.data(), e->ASZP * 4, hipMemcpyHostToDevice, e->st));
   HIPC(hipMemcpyAsync(e->hl + ent, &hv, 2, hipMemcpyHostToDevice, e->st));
+  e->rows2_stale = true;
   HIPC(launch_own_rows(*e, nullptr, nullptr));
   HIPC(launch_clear_slot_masks(*e, node, bucket, 0xFFFFFFFFu));
   HIPC(hipStreamSynchronize(e->st));
@@ -836,6 +839,62 @@ int gs_record_round(gs_engine* eh) {
   return do_stats(e, 0);
 }
 
+// The fused round with its rotation ahead (Engine::rot_ahead_ok): rotation `round` runs
+// in workgroup 0 of the round kernel into the other row buffer, concurrently with the
+// slots' workgroups on the current one, and the buffers swap after the launch (no rotation
+// launch, nothing between two round kernels).
+static int ensure_rot_ahead(Engine* e) {
+  if (e->peers2) return GS_OK;
+  const size_t N = e->N;
+  if (int s = dalloc(*e, &e->peers2, N * NB * e->ASZP, 0)) return s;
+  if (int s = dalloc(*e, &e->hl2, N * NB, 0)) return s;
+  if (int s = dalloc(*e, &e->rot_list_b[1], N, 0)) return s;
+  if (int s = dalloc(*e, &e->rot_changed_b[1], N * NB, 0)) return s;
+  e->rot_list_b[0] = e->rot_list;
+  e->rot_changed_b[0] = e->rot_changed;
+  e->rows2_stale = true;
+  return GS_OK;
+}
+
+static int round_ahead(Engine* e, uint32_t round, bool rec) {
+  if (int s = ensure_rot_ahead(e)) return s;
+  if (e->rows2_stale) {  // (first round, or the rows changed in place since)
+    HIPC(hipMemcpyAsync(e->peers2, e->peers, (size_t)e->N * NB * e->ASZP * 4, hipMemcpyDeviceToDevice, e->st));
+    HIPC(hipMemcpyAsync(e->hl2, e->hl, (size_t)e->N * NB * 2, hipMemcpyDeviceToDevice, e->st));
+    e->rows2_stale = false;
+    e->rows2_pending = -1;
+  }
+  const uint32_t par = round & 1u;
+  RotAhead ra;
+  ra.peers2 = e->peers2;
+  ra.hl2 = e->hl2;
+  // the list / changed-bit buffers the round kernel's clear does not read (it reads the last rotation's)
+  ra.list = e->rot_list == e->rot_list_b[0] ? e->rot_list_b[1] : e->rot_list_b[0];
+  ra.changed = e->rot_changed == e->rot_changed_b[0] ? e->rot_changed_b[1] : e->rot_changed_b[0];
+  ra.count = e->rot_count + par;
+  ra.plist = e->rows2_pending >= 0 ? e->rot_list : nullptr;  // the previous ahead rotation's nodes
+  ra.pcount = e->rot_count + (e->rows2_pending >= 0 ? (uint32_t)e->rows2_pending : 0u);
+  ra.round = round;
+  hipEvent_t t0;
+  e->tbegin("round", &t0);
+  const bool clr = e->rot_clear_pending;  // the last rotation's clear runs inside the round kernel
+  hipError_t r = launch_round_wg(*e, rec, e->sum_used, clr, &ra);
+  e->tend("round", t0);
+  HIPC(r);
+  std::swap(e->peers, e->peers2);
+  std::swap(e->hl, e->hl2);
+  e->rows2_pending = (int)par;
+  e->rot_list = ra.list;
+  e->rot_changed = ra.changed;
+  e->rot_parity = par;
+  e->rot_have_prev = true;
+  e->rot_clear_pending = true;
+  e->rot_cnt_dirty = true;  // (the other counter was not zeroed)
+  e->inb_valid = false;
+  if (rec && ++e->sum_used == e->sum_cap) return drain_summaries(e);
+  return GS_OK;
+}
+
 int gs_round(gs_engine* eh, uint32_t round, int record) {
   ENGINE(eh);
   if (int s = refuse_part(e)) return s;
@@ -843,6 +902,7 @@ int gs_round(gs_engine* eh, uint32_t round, int record) {
   const bool rec = record != 0;
   if (e->fused) {  // BFS + consume + prune + statistics in one kernel per slot
     if (round >= (1u << 27)) return fail(GS_ERANGE, "round index must be < 2^27");
+    if (e->rot_ahead_ok && !(e->rot_have_prev && (round & 1u) == e->rot_parity)) return round_ahead(e, round, rec);
     hipEvent_t t0;
     e->tbegin("round", &t0);
     const bool clr = e->rot_clear_pending;  // the last rotation's clear runs inside the round kernel

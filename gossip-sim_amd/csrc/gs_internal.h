@@ -161,6 +161,21 @@ struct Engine {
   bool rot_clear_pending = false;   // the last rotation's prune-bit clear is still to be applied
   bool rot_have_prev = false;
   uint32_t rot_parity = 0;          // parity of the last rotation's round
+  // Rotation ahead (round 5; fused round, N <= 16,384): rotation r runs in workgroup 0 of
+  // the round kernel r, into the OTHER row buffer (peers2 / hl2), while the slots'
+  // workgroups read the current one -- the rows change only by rotation, which depends on
+  // (seed, node, round) and the rows, not on the round's BFS or prunes -- and the buffers
+  // swap after the round. rot_list / rot_changed alternate between two buffers so the
+  // round kernel's deferred clear of the previous rotation is not overwritten.
+  bool rot_ahead_ok = false;        // enabled at create; off for good once a step API runs
+  bool rows2_stale = true;          // peers2 / hl2 need a full copy of peers / hl
+  bool rot_cnt_dirty = false;       // an ahead rotation did not zero the other counter
+  int rows2_pending = -1;           // parity of the rotation applied to peers but not peers2
+  uint32_t* peers2 = nullptr;
+  uint16_t* hl2 = nullptr;
+  uint32_t* rot_list_b[2] = {nullptr, nullptr};
+  uint32_t* rot_changed_b[2] = {nullptr, nullptr};
+
   size_t rwg_attr_lds = 0;          // dynamic LDS the round kernel was last configured for
   bool rwg_attr_prof = false;       // ... and for which instantiation (phase clocks or not)
   // node-range partition (gs_partition.hip): this rank owns node ids [part_lo, part_hi)
@@ -296,6 +311,17 @@ hipError_t mvx_apply(Engine& e, uint32_t g, uint32_t d, const unsigned long long
 hipError_t mvx_gather_consume(Engine& e, uint32_t g, bool record);
 // own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);
+// the rotation that runs inside the fused round kernel (its workgroup 0) on the other row buffer
+struct RotAhead {
+  uint32_t* peers2;
+  uint16_t* hl2;
+  uint32_t* list;            // this rotation's rotating nodes ...
+  uint32_t* count;           // ... their number ...
+  uint32_t* changed;         // ... and each rotated entry's replaced ring slots
+  const uint32_t* plist;     // the previous ahead rotation's nodes (to copy first; null: none)
+  const uint32_t* pcount;
+  uint32_t round;
+};
 hipError_t launch_consume_prune(Engine& e, bool consume, bool prune, bool apply, bool record);
 hipError_t launch_consume_prune_g(Engine& e, bool record, bool consume = true, bool zero_slot_prunes = false);
 // node-range partition (gs_partition.hip)
@@ -312,7 +338,7 @@ hipError_t launch_part_dense_apply(Engine& e, const uint32_t* dense);  // masks 
 hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear);
 hipError_t launch_rotate_clear(Engine& e);
 hipError_t launch_stats(Engine& e, uint32_t rec_index, int mode);
-hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_index, bool rot_clear);
+hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_index, bool rot_clear, const RotAhead* ra = nullptr);
 size_t round_wg_lds_bytes(uint32_t N, uint32_t fcap, uint32_t ASZP);
 size_t bfs_wg_lds_bytes(uint32_t N);
 hipError_t launch_gather_strided_u32(Engine& e, const uint32_t* src, size_t stride, uint32_t n, uint32_t* dst);

@@ -114,6 +114,7 @@ __global__ __launch_bounds__(256) void k_init_entries(const uint8_t* __restrict_
 
 hipError_t launch_init_entries(Engine& e) {
   const uint32_t total = e.N * NB;
+  e.rows2_stale = true;
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL(k_init_entries<A>, dim3(grid_for(total, 256)), dim3(256), 0, e.st,
                                               e.bucket, e.P, e.IX, e.peers, e.hl, e.N, e.ASZ, e.prm.seed));
   hipError_t r = hipGetLastError();
@@ -180,66 +181,6 @@ __global__ __launch_bounds__(1024) void k_rotate_decide(uint32_t N, uint64_t see
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) rot_list[lbase + i] = lids[i];
     __syncthreads();
   }
-}
-
-// One thread per (rotating node, entry k). On a full entry the reference's loop
-// appends the first drawn peer that is not present, draws once more and breaks,
-// then drops the oldest: the ring's head slot is overwritten.
-// (rotating node rot_list[gid / NB], entry gid % NB): PushActiveSetEntry::rotate.
-template <int ASZP>
-__device__ inline void rotate_entry(const uint8_t* __restrict__ bucket, const uint64_t* __restrict__ P,
-                                    const uint32_t* __restrict__ IX, uint32_t* __restrict__ peers,
-                                    uint16_t* __restrict__ hl, const uint32_t* __restrict__ rot_list,
-                                    uint32_t* __restrict__ rot_changed, uint32_t N, uint32_t size, uint64_t seed,
-                                    uint32_t round, uint32_t gid) {
-    const uint32_t i = gid / NB, k = gid % NB;
-  const uint32_t u = rot_list[i];
-  const uint32_t ent = u * NB + k;
-  const uint16_t hv = hl[ent];
-  uint32_t head = hv & 0xFF, L = hv >> 8;
-  const uint32_t S = size;
-  uint32_t* row = peers + (size_t)ent * ASZP;
-  const uint64_t* Pk = P + (size_t)k * (N + 1);
-  const uint32_t LX = ix_log(N);
-  const uint32_t* IXk = IX + (size_t)k * ix_count(N);
-  constexpr int R = ASZP + 2;
-  uint32_t rem[R];
-  uint64_t remw[R];
-  int nr = 0;
-  const uint64_t wself = weight(k, bucket[u]);
-  rem_insert(rem, remw, nr, u, wself);
-  const uint64_t total = Pk[N];
-  uint64_t left = total - wself;
-  Philox s(seed, P_ROTATE, u, (round << 5) | k);
-  uint32_t changed = 0;
-  for (uint32_t drawn = 0; drawn + 1 < N; ++drawn) {
-    const uint64_t v = sample_below(left, s);
-    const uint32_t c = shuffle_pick(Pk, IXk, LX, total, v, rem, remw, nr);
-    const uint64_t wc = weight(k, bucket[c]);
-    left -= wc;
-    if (nr < R) rem_insert(rem, remw, nr, c, wc);
-    bool present = false;
-    for (uint32_t j = 0; j < L; ++j) {
-      uint32_t slot = head + j;
-      if (slot >= S) slot -= S;
-      present |= row[slot] == c;
-    }
-    if (present) continue;
-    if (L < S) {
-      uint32_t slot = head + L;
-      if (slot >= S) slot -= S;
-      row[slot] = c;
-      ++L;
-      changed |= 1u << slot;
-      continue;
-    }
-    row[head] = c;
-    changed |= 1u << head;
-    head = head + 1 == S ? 0 : head + 1;
-    break;
-  }
-  hl[ent] = (uint16_t)((L << 8) | head);
-  rot_changed[ent] = changed;
 }
 
 template <int ASZP>
@@ -352,7 +293,10 @@ hipError_t launch_rotate(Engine& e, uint32_t round, bool defer_clear) {
   static const bool rot_split = std::getenv("GS_ROT_SPLIT") && std::getenv("GS_ROT_SPLIT")[0] == '1';
   const uint32_t par = round & 1u;
   uint32_t* cnt = e.rot_count + par;
-  if (e.rot_have_prev && par == e.rot_parity) {  // rounds not consecutive: this counter was not pre-zeroed
+  e.rows2_stale = true;  // (the rows change in place: a later ahead rotation copies them whole first)
+  if (e.rot_cnt_dirty || (e.rot_have_prev && par == e.rot_parity)) {  // not pre-zeroed (rounds not
+                                                                      // consecutive, or after an ahead rotation)
+    e.rot_cnt_dirty = false;
     hipError_t r = hipMemsetAsync(cnt, 0, sizeof(uint32_t), e.st);
     if (r != hipSuccess) return r;
   }

@@ -90,6 +90,22 @@ struct RoundArgs {
   const uint32_t* rot_list;
   const uint32_t* rot_count;
   const uint32_t* rot_changed;
+  // rotation ahead (rot_on): workgroup 0 runs Cluster::chance_to_rotate of round rround on
+  // the other row buffer (rpeers / rhl), after copying the previous ahead rotation's
+  // entries (plist / pcount) into it from the current one
+  uint32_t rot_on;
+  const uint64_t* P;
+  const uint32_t* IX;
+  uint32_t* rpeers;
+  uint16_t* rhl;
+  uint32_t* rlist;
+  uint32_t* rcount;
+  uint32_t* rchanged;
+  const uint32_t* plist;
+  const uint32_t* pcount;
+  uint64_t seed;
+  double rp;
+  uint32_t rround;
   uint32_t* err;
   unsigned long long* phase_clk;  // optional: per-phase clock sums (thread 0 of each workgroup)
   uint32_t wave_c_max;            // in-degree bound of the wave consume path (64; 24 for path coverage)
@@ -613,6 +629,38 @@ __device__ inline void compact_push(const uint32_t (&row)[ASZP], uint32_t pushm,
 
 // PROF: the phase clocks (GS_PHASE_PROFILE) are compiled in -- only for the C2 shape's
 // instantiation; their long-lived 64-bit clock state spilled to scratch in every build.
+// Workgroup 0 of a round kernel with rotation ahead: the previous ahead rotation's nodes'
+// entries copied from the current row buffer into the other one (which then equals the
+// current rows), then this round's rotation (decide, gossip.rs:739-754; rotate_entry,
+// push_active_set.rs:73-114,153-187) on the other buffer. The slots' workgroups only read
+// the current buffer, so the two never touch the same rows.
+template <int ASZP>
+__device__ void rotate_ahead_wg(const RoundArgs& a, uint32_t* lids) {
+  __shared__ uint32_t lcount;
+  const uint32_t tid = threadIdx.x, T = blockDim.x, N = a.N;
+  if (a.plist) {
+    const uint32_t total = *a.pcount * NB;
+    for (uint32_t gid = tid; gid < total; gid += T) {
+      const uint32_t ent = a.plist[gid / NB] * NB + gid % NB;
+#pragma unroll
+      for (int w = 0; w < ASZP; ++w) a.rpeers[(size_t)ent * ASZP + w] = a.peers[(size_t)ent * ASZP + w];
+      a.rhl[ent] = a.hl[ent];
+    }
+  }
+  if (tid == 0) lcount = 0;
+  __syncthreads();
+  for (uint32_t u = tid; u < N; u += T) {
+    Philox s(a.seed, P_DECIDE, u, a.rround);
+    if (unit_f64(s.next()) < a.rp) lids[atomicAdd(&lcount, 1u)] = u;
+  }
+  __syncthreads();  // (also: the copied rows are visible to the workgroup's rotate_entry loads)
+  const uint32_t n = lcount;
+  for (uint32_t i = tid; i < n; i += T) a.rlist[i] = lids[i];
+  if (tid == 0) *a.rcount = n;
+  for (uint32_t gid = tid; gid < n * NB; gid += T)
+    rotate_entry<ASZP>(a.bucket, a.P, a.IX, a.rpeers, a.rhl, lids, a.rchanged, N, a.ASZ, a.seed, a.rround, gid);
+}
+
 template <int ASZP, bool OFF16, int FP, bool PROF>
 __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundArgs a) {
   using PMT = typename std::conditional<(ASZP <= 16), uint16_t, uint32_t>::type;
@@ -640,7 +688,11 @@ __global__ __launch_bounds__(RWG_THREADS, RWG_MIN_WAVES) void k_round_wg(RoundAr
   uint32_t* scr = reinterpret_cast<uint32_t*>(smem + L.scr) + wid * RWG_SCR;
   const uint32_t W = (N + 31) / 32;
 
-  const uint32_t o = blockIdx.x;
+  if (a.rot_on && blockIdx.x == 0) {  // (dispatched first: the rotation overlaps the whole round)
+    rotate_ahead_wg<ASZP>(a, reinterpret_cast<uint32_t*>(smem));
+    return;
+  }
+  const uint32_t o = blockIdx.x - a.rot_on;
   const uint32_t org = a.origin[o], ob = a.obkt[o], nf = a.nfail[o];
   const size_t base = (size_t)o * N;
   uint32_t errf = 0;
@@ -1066,7 +1118,7 @@ static hipError_t launch_rwg_p(Engine& e, const RoundArgs& a, size_t lds) {
     e.rwg_attr_lds = lds;
     e.rwg_attr_prof = PROF;
   }
-  hipLaunchKernelGGL((k_round_wg<ASZP, OFF16, FP, PROF>), dim3(e.S), dim3(RWG_THREADS), lds, e.st, a);
+  hipLaunchKernelGGL((k_round_wg<ASZP, OFF16, FP, PROF>), dim3(e.S + a.rot_on), dim3(RWG_THREADS), lds, e.st, a);
   return hipSuccess;
 }
 
@@ -1086,8 +1138,14 @@ static hipError_t launch_rwg(Engine& e, const RoundArgs& a, size_t lds) {
   return launch_rwg_fp<ASZP, OFF16, ASZP>(e, a, lds);
 }
 
-hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_slot, bool rot_clear) {
+hipError_t launch_round_wg(Engine& e, bool record, uint32_t rec_slot, bool rot_clear, const RotAhead* ra) {
   RoundArgs a;
+  a.rot_on = ra ? 1u : 0u;
+  a.P = e.P; a.IX = e.IX; a.seed = e.prm.seed; a.rp = e.prm.rotation_probability;
+  a.rpeers = ra ? ra->peers2 : nullptr; a.rhl = ra ? ra->hl2 : nullptr;
+  a.rlist = ra ? ra->list : nullptr; a.rcount = ra ? ra->count : nullptr; a.rchanged = ra ? ra->changed : nullptr;
+  a.plist = ra ? ra->plist : nullptr; a.pcount = ra ? ra->pcount : nullptr;
+  a.rround = ra ? ra->round : 0u;
   a.stake = e.stake; a.bucket = e.bucket; a.peers = e.peers; a.hl = e.hl; a.frank = e.frank; a.srank = e.srank;
   a.by_srank = e.by_srank; a.prank = e.prank; a.by_prank = e.by_prank; a.pstake = e.pstake; a.rinfo = e.rinfo; a.origin = e.origin;
   a.obkt = e.obkt; a.nfail = e.nfail; a.min_ingress = e.min_ingress; a.thr = e.thr; a.slot_prunes = e.slot_prunes;
