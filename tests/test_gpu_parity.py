@@ -317,6 +317,56 @@ def test_fused_round_matches_steps(mode, narrow):
     np.testing.assert_array_equal(a.summaries(), b.summaries())
 
 
+def test_rotation_ahead_matches_serial_rotation(monkeypatch):
+    """The one-kernel round with its rotation run ahead in the round kernel's workgroup 0 on
+    a second row buffer (round 5, the default) == the same engine with GS_ROT_AHEAD=0 (a
+    rotation launch after each round), through the state changes the double buffer must
+    survive: consecutive rounds, a repeated round parity (serial fallback), step-wise calls
+    including a step rotation, an uploaded entry, and ahead rounds again. Rotation
+    probability 0.2 so that ~80 of 400 nodes rotate per round."""
+    pks, st = eb.synth.network(400)
+    engs = []
+    for ahead in (True, False):
+        if ahead:
+            monkeypatch.delenv("GS_ROT_AHEAD", raising=False)
+        else:
+            monkeypatch.setenv("GS_ROT_AHEAD", "0")
+        e = gs.Engine(st, 5, seed=11, rotation_probability=0.2, bfs_mode=gs.GS_BFS_WORKGROUP)
+        e.set_slots([0, 3, 50, 150, 399], [2, 0, 2, 1, 2], [0.15, 0.0, 0.5, 0.05, 0.15])
+        e.init_active_sets()
+        engs.append(e)
+    monkeypatch.delenv("GS_ROT_AHEAD", raising=False)
+
+    def both(f):
+        for e in engs:
+            f(e)
+
+    for r in range(8):
+        both(lambda e: e.round(r, record=r >= 2))
+    both(lambda e: e.round(9, record=True))   # same parity as round 7: serial fallback
+    both(lambda e: e.round(10, record=True))
+    both(lambda e: (e.run_gossip(), e.consume_messages(), e.send_prunes(), e.prune_connections(),
+                    e.chance_to_rotate(11)))  # step-wise, with an in-place rotation
+    for r in range(12, 16):
+        both(lambda e: e.round(r, record=True))
+    peers = engs[1].get_entry(7, 3)
+    both(lambda e: e.set_entry(7, 3, peers[::-1]))  # an uploaded entry (rows change in place)
+    for r in range(16, 24):  # through the first prune wave
+        both(lambda e: e.round(r, record=True))
+    a, b = engs
+    pa, la = a.active_sets()
+    pb, lb = b.active_sets()
+    np.testing.assert_array_equal(la, lb)
+    np.testing.assert_array_equal(pa, pb)
+    for k in range(5):
+        np.testing.assert_array_equal(a.hops(k), b.hops(k))
+        np.testing.assert_array_equal(a.pruned_all(k), b.pruned_all(k))
+        for x, y in zip(a.caches(k), b.caches(k)):
+            np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(a.summaries(), b.summaries())
+    assert a.info()["bfs_mode"] == b.info()["bfs_mode"]
+
+
 @pytest.mark.parametrize("narrow", [False, True])
 def test_multi_fused_gather_consume_matches_steps(narrow, monkeypatch):
     """GS_MV_FUSED=1: the multi-source BFS's gs_round consumes straight from the gather's
