@@ -226,6 +226,11 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
     eng.close()
     mode = {2: "level", 3: "binned", 4: "multi"}.get(info["bfs_mode"], str(info["bfs_mode"]))
     bp = b_prop(V, E, args.active_set_size)
+    # committed PMC / trace summaries are of the 13-slot configuration: a share run
+    # (--c4-sims) looks them up under its own slot set, so it never reports another
+    # configuration's traffic (null unless a summary of that share exists)
+    tag = f"bfs_{mode}_c4" + (f"_s{args.c4_sims.replace(',', '-')}" if args.c4_sims else "")
+    pers = info.get("bfs_persistent", False)
     return {"workload": f"C4: {nodes}-node power-law network, origin rank 1, fail-nodes 0.1..0.5 (when-to-fail 0) + "
                         f"prune-stake-threshold 0.05..0.40: {S} sims as slots of one engine",
             "bfs_mode": mode, "rounds": [warmup, warmup + steps], "ms_per_step": dt / steps * 1e3,
@@ -237,10 +242,11 @@ def c4_leg(gs, synth, args, nodes=1_000_000, warmup=5, steps=20):
             # multi: the level loop plus the gather that writes hops / in-degrees / inbound rows
             # (with GS_MV_FUSED=1 the gather runs fused with consume, and its whole time is charged)
             "bfs_roofline": roofline(bp, fam["bfs"] + fam.get("gather", 0.0) + fam.get("gather_consume", 0.0), steps,
-                                     f"BFS ({mode}: " + ("expand/apply per level + " +
-                                                         ("fused gather/consume)" if "gather_consume" in fam
-                                                          else "gather)") if mode == "multi" else "per level)"),
-                                     "B_prop (SURVEY 8d), summed over slots", f"bfs_{mode}_c4")}
+                                     f"BFS ({mode}: " + (("one persistent launch" if pers else "expand/apply per level")
+                                                         + " + " + ("fused gather/consume)" if "gather_consume" in fam
+                                                                    else "gather)") if mode == "multi"
+                                                         else "per level)"),
+                                     "B_prop (SURVEY 8d), summed over slots", tag)}
 
 
 def gather_phases(eng):

@@ -263,13 +263,15 @@ class Engine:
         pb, ob = C.c_uint64(), C.c_uint64()
         _check(lib().gs_engine_memory(self.h, C.byref(pb), C.byref(ob)))
         return {"n_nodes": n.value, "n_slots": s.value, "bfs_mode": m.value, "device_bytes": b.value,
-                "pair_bytes": pb.value, "other_bytes": ob.value, "fused_round": bool(f.value)}
+                "pair_bytes": pb.value, "other_bytes": ob.value, "fused_round": bool(f.value),
+                "bfs_persistent": bool(self.bfs_geometry()["persistent_wgs"])}
 
     def bfs_geometry(self):
         """Multi / hybrid BFS geometry (diagnostics): expand slice, coarse and fine bins, group width, groups."""
-        out = np.zeros(5, dtype=np.uint32)
-        _check(lib().gs_engine_bfs_geometry(self.h, _ptr(out), 5))
-        return dict(zip(["expand_slice", "coarse_bins", "fine_bins", "group_width", "groups"], out.tolist()))
+        out = np.zeros(6, dtype=np.uint32)
+        _check(lib().gs_engine_bfs_geometry(self.h, _ptr(out), 6))
+        return dict(zip(["expand_slice", "coarse_bins", "fine_bins", "group_width", "groups", "persistent_wgs"],
+                        out.tolist()))
 
     def set_slots(self, origins, min_ingress=2, thresholds=0.15):
         S = self.n_slots

@@ -1529,11 +1529,15 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     }
     hipEvent_t t0;
     e.tbegin("bfs", &t0);
-    if (!e.mv_vis_clean && (r = hipMemsetAsync(e.mv_vis, 0, (size_t)e.N * 4, e.st))) return r;
-    e.mv_vis_clean = false;
+    // the persistent BFS (gs_bfs_pers.hip) keeps the visited masks in LDS: vis stays as it is
+    const bool pers = pb_usable(e) && !e.mv_diag;
+    if (!pers && !e.mv_vis_clean && (r = hipMemsetAsync(e.mv_vis, 0, (size_t)e.N * 4, e.st))) return r;
+    if (!pers) e.mv_vis_clean = false;
     uint32_t nlev = 254;  // (the gather reads the levels' sizes; empty levels end the BFS)
     const std::vector<uint32_t>& pv = e.mv_pred[g];
-    if (pv.empty() || polled_only || e.mv_diag) {
+    if (pers) {
+      if ((r = launch_bfs_pers(e, a, gr))) return r;
+    } else if (pv.empty() || polled_only || e.mv_diag) {
       if ((r = mv_group_polled(e, a, gr, lag, nlev))) return r;
       if (!polled_only) {  // this round's sizes seed the prediction
         // (levels enqueued after the one that ended the BFS may not have run yet: PENDING = 0)
@@ -1572,10 +1576,10 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     e.tbegin(consume ? "gather_consume" : "gather", &t0);
     // an unpartitioned engine's fine bins cover every node: the gather leaves vis zeroed
     // for the next BFS (one memset launch less per group and round)
-    a.clear_vis = e.part_on ? 0u : 1u;
+    a.clear_vis = e.part_on || pers ? 0u : 1u;
     if (consume) hipLaunchKernelGGL(k_mv_consume, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a);
     else hipLaunchKernelGGL(k_mv_gather, dim3(ggrid), dim3(MV_GT), lds_g, e.st, a);
-    e.mv_vis_clean = a.clear_vis != 0;
+    if (!pers) e.mv_vis_clean = a.clear_vis != 0;
     e.tend(consume ? "gather_consume" : "gather", t0);
     if (e.mv_diag) {  // GS_MV_DIAG=1: entries and records of the group's BFS (diagnostics)
       std::vector<uint32_t> pu(fno);

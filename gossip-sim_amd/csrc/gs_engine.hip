@@ -126,6 +126,7 @@ static void destroy_engine(Engine* e) {
   if (e->x_pin) hipHostFree(e->x_pin);
   if (e->mv_hlvl) hipHostFree(e->mv_hlvl);
   if (e->mv_prof) hipHostFree(e->mv_prof);
+  if (e->pb_registered) pb_register(*e, false);
   for (auto& kv : e->timers)
     for (auto& pr : kv.second.ev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (hipEvent_t x : e->ev_pool) hipEventDestroy(x);
@@ -461,6 +462,16 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
       ALLOC(e->mv_pused, fno, 0);
       ALLOC(e->mv_bar, 256, 0);  // the persistent level kernel's barrier words (MV_BAR_WORDS)
       e->pair_bytes += e->dev_bytes - b0;
+      if (pb_setup(*e)) {  // the persistent BFS (gs_bfs_pers.hip): its level records, T rows and entries
+        ALLOC(e->pb_T[0], (size_t)(e->pb_G + 2) * e->pb_rows_cap, 0);
+        ALLOC(e->pb_T[1], (size_t)(e->pb_G + 2) * e->pb_rows_cap, 0);
+        ALLOC(e->pb_area[0], e->pb_area_cap, 0);
+        ALLOC(e->pb_area[1], e->pb_area_cap, 0);
+        ALLOC(e->pb_blk, pb_blk_words(), 0);
+        ALLOC(e->pb_gq, (size_t)e->pb_G * e->pb_gq_cap, 0);
+        pb_register(*e, true);
+        e->pb_registered = true;
+      }
     }
     ALLOC(e->mv_fcls, N, 0xFF);
     ALLOC(e->mv_fk, S, 0);
@@ -1303,6 +1314,7 @@ int gs_engine_bfs_geometry(gs_engine* eh, uint32_t* out, size_t n) {
   out[2] = on ? e->mv.nbf : 0;
   out[3] = on ? e->mv.GW : 0;
   out[4] = on ? (uint32_t)e->mv_groups.size() : 0;
+  if (n >= 6) out[5] = pb_usable(*e) ? e->pb_G : 0;  // workgroups of the persistent BFS (0: launched level loop)
   return GS_OK;
 }
 

@@ -153,6 +153,15 @@ struct Engine {
   unsigned long long* hb_pgr = nullptr;  // [nbc][hb_bin_cap] in-records src | slot mask << 32
   size_t hb_bin_cap = 0;
   uint32_t hb_parts = 0, hb_slices = 0;  // T rows per slice (entries per node at most), slices
+  // persistent multi-source BFS (gs_bfs_pers.hip, round 6): one launch per slot group,
+  // G workgroups (one per CU) that own interleaved fine bins; off on partition ranks
+  bool pb_on = false, pb_registered = false;
+  uint32_t pb_G = 0, pb_GL = 0, pb_FPW = 0, pb_LB = 0, pb_CH = 0, pb_rows_cap = 0, pb_gq_cap = 0;
+  size_t pb_lds = 0, pb_attr_lds = 0, pb_area_cap = 0;
+  uint32_t* pb_T[2] = {nullptr, nullptr};              // per level parity: [G + 2][rows_cap] T rows
+  unsigned long long* pb_area[2] = {nullptr, nullptr}; // per level parity: records [area_cap]
+  uint32_t* pb_blk = nullptr;                          // barrier + per-level slice counters
+  uint2* pb_gq = nullptr;                              // [G][gq_cap] level entries beyond the LDS list
   std::vector<uint32_t> h_nfail_any;  // host copy: slot has failed nodes
   // rotation
   uint32_t* rot_list = nullptr;
@@ -303,6 +312,12 @@ void hb_geometry(Engine& e, uint32_t parts);  // area / T rows / in-record regio
 // the multi-source BFS's layout (node-major masks and egress, slot groups): MULTI and HYBRID
 inline bool mv_layout(const Engine& e) { return e.bfs_mode == GS_BFS_MULTI || e.bfs_mode == GS_BFS_HYBRID; }
 hipError_t mv_update_failures(Engine& e, const std::vector<uint32_t>& nf);
+// persistent multi-source BFS (gs_bfs_pers.hip): geometry at create (false: not usable),
+// the process-wide count of engines that may launch it, and whether it runs now
+bool pb_setup(Engine& e);
+void pb_register(Engine& e, bool on);
+bool pb_usable(const Engine& e);
+size_t pb_blk_words();
 // frontier-exchange partition levels (gs_bfs_multi.hip): seed, expand + pack, apply, gather
 hipError_t mvx_begin(Engine& e, uint32_t g, uint32_t& n_local);
 hipError_t mvx_expand(Engine& e, uint32_t g, uint32_t d, uint32_t n_local, std::vector<uint64_t>& words_to);

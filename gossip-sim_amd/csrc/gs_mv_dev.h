@@ -316,4 +316,7 @@ __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_b
 // Kernel arguments of slot group g (gs_bfs_multi.hip).
 MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g);
 
+// The whole BFS of one slot group as one persistent launch (gs_bfs_pers.hip).
+hipError_t launch_bfs_pers(Engine& e, const MvArgs& a, const MvGroup& gr);
+
 }  // namespace gs

@@ -202,7 +202,9 @@ int gs_engine_memory(gs_engine* e, uint64_t* pair_bytes, uint64_t* other_bytes);
 int gs_engine_round_kind(gs_engine* e, uint32_t* fused);
 /* Geometry of the multi-source / hybrid BFS (diagnostics; not a reference interface): out[0]
  * frontier entries (multi) or nodes (hybrid) per expand slice, out[1] coarse destination bins,
- * out[2] fine bins, out[3] slots per slot group, out[4] slot groups. n >= 5; zeros in other modes. */
+ * out[2] fine bins, out[3] slots per slot group, out[4] slot groups; with n >= 6, out[5] the
+ * workgroups of the persistent BFS launch (0: the launched level loop runs). n >= 5; zeros in
+ * other modes. */
 int gs_engine_bfs_geometry(gs_engine* e, uint32_t* out, size_t n);
 
 /* --- node-range partition ------------------------------

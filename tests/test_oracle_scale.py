@@ -197,9 +197,43 @@ def test_c4_sweep_semantics_match_oracle_100k(case, monkeypatch):
     caches and the per-round summaries' integer fields. The c5 case runs C5's slot shape
     (eight distinct origins) through the multi BFS's wide-geometry paths at 40k nodes."""
     n, slots, mode, env = SWEEP_CASES[case]
+    sweep_vs_oracle(n, slots, mode, env, monkeypatch)
+
+
+def test_c4_slots_match_oracle_1m(monkeypatch):
+    """Whole rounds at the north star's size: BASELINE C4's 1M-node network with two of its
+    13 sweep sims as the slots of one engine -- fail-nodes 0.3 (when-to-fail 0) and
+    prune-stake threshold 0.40 -- through gs_round (the production path: the multi-source
+    BFS, its gather, k_cg_consume, k_cg_prune, the statistics kernels) for 22 rounds, through
+    the first prune wave, against two oracle sims that hold the engine's active sets and run
+    the reference's rounds themselves (gossip.rs:494-737, received_cache.rs:38-131): failed
+    sets, hops, inbound (src, hop) lists, prunes, counters, prune state, received caches (every
+    fourth round and the wave) and the round summaries' integers."""
+    slots = [(1, 0.3, 0.15, 2), (1, 0.0, 0.40, 2)]
+    sweep_vs_oracle(1_000_000, slots, gs.GS_BFS_MULTI, {}, monkeypatch, full_every=4)
+
+
+def test_rounds_with_rotation_match_oracle_100k(monkeypatch):
+    """Rotation inside whole-round parity at 100k nodes: rotation probability 0.002 (about 200
+    nodes rotate per round), so after the first prune wave rotated entries drop the replaced
+    ring slot's prune filter while the retained peers keep theirs (Cluster::chance_to_rotate
+    gossip.rs:739-754 -> PushActiveSet::rotate push_active_set.rs:153-187: the new key gets a
+    fresh filter, shift_remove_index(0) drops the oldest key's). The oracle sims get the
+    engine's active sets once (after initialize_gossip) and then rotate on their own (the
+    same Philox DECIDE / ROTATE streams, the determinism contract); the engine runs gs_round
+    (multi BFS, rotation fused into one launch above 16K nodes, the deferred prune-bit clear).
+    Two slots (a failure slot, a threshold slot), 24 rounds: everything the sweep test
+    compares, plus the active sets of every rotated node each round."""
+    slots = [(1, 0.1, 0.15, 2), (2, 0.0, 0.30, 3)]
+    sweep_vs_oracle(100_000, slots, gs.GS_BFS_MULTI, {}, monkeypatch, rounds=24, p=0.002, check_rotation=True)
+
+
+def sweep_vs_oracle(n, slots, mode, env, monkeypatch, rounds=22, p=0.0, full_every=5, check_rotation=False):
+    """One engine with `slots` = [(origin stake rank, fail fraction, threshold, min-ingress)]
+    run by gs_round against one oracle sim per slot (see the tests above)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    seed, rounds = 0x5EED0011, 22
+    seed, asz = 0x5EED0011, 12
     st = eb.synth.power_law_stakes(n)
     rank_order = np.lexsort((np.arange(n), -st.astype(np.float64)))
     S = len(slots)
@@ -207,7 +241,7 @@ def test_c4_sweep_semantics_match_oracle_100k(case, monkeypatch):
     fr = [f for _, f, _, _ in slots]
     thr = [t for _, _, t, _ in slots]
     mi = [m for _, _, _, m in slots]
-    eng = gs.Engine(st, S, rotation_probability=0.0, seed=seed, bfs_mode=mode)
+    eng = gs.Engine(st, S, rotation_probability=p, seed=seed, bfs_mode=mode, active_set_size=asz)
     for k in env:
         monkeypatch.delenv(k)
     if "GS_MV_BSC" in env:
@@ -225,13 +259,15 @@ def test_c4_sweep_semantics_match_oracle_100k(case, monkeypatch):
 
     with ThreadPoolExecutor(max_workers=S) as ex:
         sims = list(ex.map(make_sim, range(S)))
-    del peers, lens
+    if not check_rotation:
+        del peers, lens
     eng.fail_nodes(fr)
     for k, s in enumerate(sims):
         np.testing.assert_array_equal(eng.failed(k), s.failed(), err_msg=f"failed set slot {k}")
     pruned_total = [0] * S
+    rotated_pruned = 0  # rotated entries whose node held prune state (the filter rule ran)
 
-    def oracle_round(k, full):  # the reference's round for slot k (the C calls release the GIL)
+    def oracle_round(k, r, full):  # the reference's round for slot k (the C calls release the GIL)
         s, o = sims[k], origins[k]
         s.run_gossip(o)
         w = {"mn": s.rmr_mn(), "stranded": len(s.stranded()), "dist": s.distances(), "orders": s.orders_all(64 * n)}
@@ -242,13 +278,16 @@ def test_c4_sweep_semantics_match_oracle_100k(case, monkeypatch):
             w["caches"] = s.caches(o)
         s.prune_connections()
         w["counters"] = s.counters()
+        if p > 0:
+            w["pruned_before_rotation"] = s.pruned_all(o)
+            s.chance_to_rotate(asz, p, r)
         w["pruned"] = s.pruned_all(o)
         return w
 
     with ThreadPoolExecutor(max_workers=S) as ex:
         for r in range(rounds):
-            full = r % 5 == 0 or 18 <= r <= 20 or r == rounds - 1
-            futs = [ex.submit(oracle_round, k, full) for k in range(S)]
+            full = r % full_every == 0 or 18 <= r <= 20 or r == rounds - 1
+            futs = [ex.submit(oracle_round, k, r, full) for k in range(S)]
             eng.round(r, record=True)
             summ_r = eng.summaries()[r]
             for k in range(S):
@@ -259,6 +298,7 @@ def test_c4_sweep_semantics_match_oracle_100k(case, monkeypatch):
                 np.testing.assert_array_equal(off, w_off, err_msg=f"in-degrees slot {k} round {r}")
                 np.testing.assert_array_equal(src[:len(w_src)], w_src, err_msg=f"inbound sources slot {k} round {r}")
                 np.testing.assert_array_equal(hop[:len(w_hop)], w_hop, err_msg=f"inbound hops slot {k} round {r}")
+                del off, src, hop, w_off, w_src, w_hop
                 pruned_total[k] += len(w["prunes"])
                 assert eng.prunes(k) == w["prunes"], f"prunes slot {k} round {r}"
                 if full:
@@ -270,11 +310,13 @@ def test_c4_sweep_semantics_match_oracle_100k(case, monkeypatch):
                     np.testing.assert_array_equal(ln, oln, err_msg=f"cache lengths slot {k} round {r}")
                     np.testing.assert_array_equal(keys, okeys, err_msg=f"cache keys slot {k} round {r}")
                     np.testing.assert_array_equal(sc, osc, err_msg=f"cache scores slot {k} round {r}")
+                    del up, ln, keys, sc, oup, oln, okeys, osc, has
                 eg, ig, pr = eng.counters(k)
                 oe, oi, op = w["counters"]
                 np.testing.assert_array_equal(eg, np.where(oe == U64MAX, 0, oe), err_msg=f"egress slot {k} round {r}")
                 np.testing.assert_array_equal(ig, np.where(oi == U64MAX, 0, oi), err_msg=f"ingress slot {k} round {r}")
                 np.testing.assert_array_equal(pr, op, err_msg=f"prune-sent slot {k} round {r}")
+                # (after the round's rotation: replaced ring slots' bits are dropped)
                 np.testing.assert_array_equal(eng.pruned_all(k), w["pruned"], err_msg=f"prune state slot {k} round {r}")
                 # the round summary's integers (gossip_main.rs:480-563): RMR m / n, stranded, prunes
                 m_, n_ = w["mn"]
@@ -282,5 +324,17 @@ def test_c4_sweep_semantics_match_oracle_100k(case, monkeypatch):
                 assert int(sm["pushes"]) == m_ and int(sm["visited"]) == n_, (k, r, sm, m_, n_)
                 assert int(sm["stranded"]) == w["stranded"], (k, r)
                 assert int(sm["prunes"]) == len(w["prunes"]), (k, r)
-    assert all(p > 0 for p in pruned_total), pruned_total  # every slot went through a prune wave
+                if check_rotation and k == 0:
+                    p2, l2 = eng.active_sets()
+                    chg = np.nonzero((p2 != peers).any(axis=(1, 2)) | (l2 != lens).any(axis=1))[0]
+                    for v in chg[:64].tolist():  # the rotated nodes' entries equal the oracle's
+                        for b in range(25):
+                            want = sims[0].entry(v, b)
+                            np.testing.assert_array_equal(p2[v, b, :l2[v, b]], want,
+                                                          err_msg=f"entry ({v}, {b}) after round {r}")
+                    rotated_pruned += int(np.count_nonzero(w["pruned_before_rotation"][chg]))
+                    peers, lens = p2, l2
+    assert all(x > 0 for x in pruned_total), pruned_total  # every slot went through a prune wave
+    if check_rotation:
+        assert rotated_pruned > 0, "no rotated node held prune state"
     eng.close()
