@@ -46,9 +46,9 @@ namespace {
 constexpr uint32_t PB_T = 1024;   // threads per workgroup (one workgroup per CU)
 constexpr uint32_t PB_SEG = 1024; // T-column slices per receive batch
 constexpr uint32_t PB_EC = 1024;  // level entries kept in LDS (beyond: the workgroup's global region)
-// control block (pb_blk): barrier shard counters at 16 s (s < 8), top counter 128,
-// generation 144; the slice counter of level L at 256 + L. Zeroed before every launch.
-constexpr uint32_t PB_BLK_WORDS = 512;
+// control block (pb_blk): barrier shard counters at 64 s (s < 8), top counter 512,
+// generation 576; the slice counter of level L at 1024 + L. Zeroed before every launch.
+constexpr uint32_t PB_BLK_WORDS = 1280;
 // dynamic LDS header: the group's slots (MvSlots), its table (GT_WORDS), 16 control words
 constexpr uint32_t PB_HDR_SLOTS = (uint32_t)((sizeof(MvSlots) + 15) & ~(size_t)15);
 constexpr uint32_t PB_HDR = PB_HDR_SLOTS + 4 * GT_WORDS + 64;
@@ -86,23 +86,25 @@ __device__ inline unsigned long long ld_agent64(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Grid barrier (counter form, sharded by blockIdx & 7): every wave drains its stores
+// Grid barrier (counter form, sharded by blockIdx & 7; every counter on a 256-B line of its
+// own: the pollers' loads do not contend with the arrivals): every wave drains its stores
 // (write-through sc1 stores and device-scope atomics: s_waitcnt vmcnt(0)) before the
 // workgroup barrier, thread 0 arrives on its shard, the last of a shard on the top
 // counter, the last shard publishes generation e; thread 0 polls it relaxed. The block is
 // zeroed before every launch, so epochs start at 1. A spin is bounded (~1 s): on expiry
 // ERR_SYNC is raised and the workgroup goes on (the engine is then refused).
+constexpr uint32_t PB_BAR_STR = 64, PB_BAR_TOP = 8 * PB_BAR_STR, PB_BAR_GEN = 9 * PB_BAR_STR, PB_SLICES = 1024;
 __device__ inline void pb_grid_sync(uint32_t* bar, uint32_t e, uint32_t G, uint32_t* err) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t sh = blockIdx.x & 7u, ns = min(G, 8u), cs = (G - sh + 7u) / 8u;
-    const uint32_t r = __hip_atomic_fetch_add(&bar[16 * sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t r = __hip_atomic_fetch_add(&bar[PB_BAR_STR * sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (r + 1u == e * cs) {
-      const uint32_t t = __hip_atomic_fetch_add(&bar[128], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t + 1u == e * ns) __hip_atomic_store(&bar[144], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t t = __hip_atomic_fetch_add(&bar[PB_BAR_TOP], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1u == e * ns) __hip_atomic_store(&bar[PB_BAR_GEN], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    for (uint32_t it = 0; __hip_atomic_load(&bar[144], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e; ++it) {
+    for (uint32_t it = 0; __hip_atomic_load(&bar[PB_BAR_GEN], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e; ++it) {
       if (it > (1u << 22)) {
         atomicOr(err, ERR_SYNC);
         break;
@@ -111,6 +113,40 @@ __device__ inline void pb_grid_sync(uint32_t* bar, uint32_t e, uint32_t G, uint3
     }
   }
   __syncthreads();
+}
+
+// mv_block_scan with LDS-only barriers: global stores in flight (T rows, records, egress)
+// are not waited for -- the grid barrier drains them once per level.
+__device__ inline uint32_t pb_block_scan(uint32_t* h, uint32_t n, uint32_t* wsum) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = PB_T >> 6;
+  const uint32_t per = (n + PB_T - 1) / PB_T;
+  const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
+  uint32_t s = 0;
+  for (uint32_t i = lo; i < hi; ++i) s += h[i];
+  const uint32_t incl = wave_incl_scan(s);
+  if (lane == 63) wsum[wid] = incl;
+  lds_barrier();
+  uint32_t wb = 0, tot = 0;
+  for (uint32_t k = 0; k < nw; ++k) {
+    if (k < wid) wb += wsum[k];
+    tot += wsum[k];
+  }
+  uint32_t run = wb + incl - s;
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t c = h[i];
+    h[i] = run;
+    run += c;
+  }
+  lds_barrier();
+  return tot;
+}
+
+__device__ inline void st_entry(uint2* p, uint2 x) {  // (sc1: read back by other waves of the workgroup)
+  st_agent64(reinterpret_cast<unsigned long long*>(p), (unsigned long long)x.x | ((unsigned long long)x.y << 32));
+}
+__device__ inline uint2 ld_entry(const uint2* p) {
+  const unsigned long long v = ld_agent64(reinterpret_cast<const unsigned long long*>(p));
+  return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
 }
 
 template <int ASZP>
@@ -126,8 +162,9 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
   const uint32_t BSF = a.BSF, BPm = (1u << BSF) - 1, UB = a.UB, LB = p.LB;
   const uint32_t FPW = p.FPW, NO = FPW << BSF, ASZ = a.ASZ, CH = p.CH;
   const unsigned long long UBm = (1ull << UB) - 1, LBm = (1ull << LB) - 1;
-  // LDS: stage [stage_cap] u64 (receive: the T column's counts and run starts) | visL [NO] |
-  // visP [NO] | hist [G + 16] | fcur [FPW, padded to 4] | ent [PB_EC] u64 | bk [NO] u8
+  // LDS: stage [stage_bytes] (expand: CH * ASZ u64 records; receive: the T column's counts and
+  // run starts, then the level's touched nodes) | visL [NO] | visP [NO] | hist [G + 16] |
+  // fcur [FPW, padded to 4] | ent [PB_EC] u64 | bk [NO] u8 | (GS_PB_TRACE table)
   unsigned long long* stage = reinterpret_cast<unsigned long long*>(smem);
   uint32_t* visL = reinterpret_cast<uint32_t*>(smem + p.stage_bytes);
   uint32_t* visP = visL + NO;
@@ -137,6 +174,7 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
   uint8_t* bk = reinterpret_cast<uint8_t*>(ent + PB_EC);
   uint32_t* pre = reinterpret_cast<uint32_t*>(stage);  // [PB_SEG + 1] (receive only)
   uint32_t* sb = pre + PB_SEG + 1;                     // [PB_SEG]
+  uint32_t* tl = sb + PB_SEG + 3;                      // [NO] nodes with new bits this level
   uint2* gq = p.gq + (size_t)g * p.gq_cap;
   auto node_of = [&](uint32_t li) { return ((((li >> BSF) << GL) + g) << BSF) | (li & BPm); };
 
@@ -149,7 +187,7 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
     bk[i] = v < a.N ? a.bucket[v] : (uint8_t)0;
   }
   for (uint32_t i = tid; i < FPW; i += PB_T) fcur[i] = 0;
-  __syncthreads();
+  lds_barrier();
   if (tid == 0) {  // level 0: the group's seeds (distinct origins, their own entries) this workgroup owns
     uint32_t n = 0;
     for (uint32_t i = 0; i < p.nseed; ++i) {
@@ -163,41 +201,57 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
     }
     sh[1] = n;
   }
-  __syncthreads();
+  lds_barrier();
   uint32_t ne = sh[1];
   uint32_t L = 0, ep = 0;
+  // GS_PB_TRACE (diagnostics): thread 0 keeps per-level phase times in LDS (u32, 10 ns units)
+  // and merges them into the global table (max over workgroups) once, after the BFS
   const bool trc = p.tr != nullptr && tid == 0;
+  uint32_t* trl = reinterpret_cast<uint32_t*>(bk + ((NO + 15) & ~15u));  // [PB_TRL][16] (trace builds only)
+  constexpr uint32_t PB_TRL = 40;
+  if (p.tr) {
+    for (uint32_t i = tid; i < PB_TRL * 16; i += PB_T) trl[i] = 0;
+    lds_barrier();
+  }
   unsigned long long t0 = trc ? wall_clock64() : 0, tm = t0;
-  auto tmark = [&](int slot, bool mx) {  // (diagnostics only)
-    if (!trc || L >= 120) return;
+  auto tmark = [&](int slot, bool mx) {
+    if (!trc || L >= PB_TRL) return;
     const unsigned long long now = wall_clock64();
-    if (mx) atomicMax(&p.tr[16 * L + slot], now - tm);
-    else if (g == 0) p.tr[16 * L + slot] = now - t0;
+    if (mx) trl[16 * L + slot] = max(trl[16 * L + slot], (uint32_t)(now - tm));
+    else trl[16 * L + slot] = (uint32_t)(now - t0);
     tm = now;
   };
   for (;;) {
     tmark(0, false);
-    if (trc && L < 120) atomicAdd(&p.tr[16 * L + 5], (unsigned long long)ne);
+    if (trc && L < PB_TRL) trl[16 * L + 5] = ne;
     // ---------------------------------------------- expand level L ----
     const uint32_t par = L & 1;
     uint32_t* T = p.T[par];
     unsigned long long* area = p.area[par];
     for (uint32_t c0 = 0; c0 < ne; c0 += CH) {  // (ne is workgroup-uniform)
-      if (tid == 0) sh[2] = atomicAdd(&p.blk[256 + L], 1u);  // the chunk's slice
+      // the chunk's slice: the returned value is first needed after the expansion (its
+      // latency overlaps the row loads)
+      uint32_t wsl = 0;
+      if (tid == 0) wsl = atomicAdd(&p.blk[PB_SLICES + L], 1u);
       for (uint32_t i = tid; i < G; i += PB_T) hist[i] = 0;
-      __syncthreads();
+      lds_barrier();
       if (c0 == 0) tmark(8, true);
       uint32_t row[ASZP], acc[ASZP], u = 0;
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
       const uint32_t i = c0 + tid;
-      if (tid < CH && i < ne) mv_expand_entry<ASZP>(a, i < PB_EC ? ent[i] : gq[i - PB_EC], S, row, acc, u);
+      if (tid < CH && i < ne) mv_expand_entry<ASZP>(a, i < PB_EC ? ent[i] : ld_entry(&gq[i - PB_EC]), S, row, acc, u);
+      if (trc && c0 == 0) {  // (trace: thread 0's own entry, its loads and stores drained)
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        tmark(7, true);
+      }
       uint32_t rk[ASZP];
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) rk[s] = acc[s] ? atomicAdd(&hist[(row[s] >> BSF) & (G - 1)], 1u) : 0u;
-      __syncthreads();
+      if (tid == 0) sh[2] = wsl;
+      lds_barrier();
       if (c0 == 0) tmark(9, true);
-      const uint32_t total = mv_block_scan(hist, G, hist + G);
+      const uint32_t total = pb_block_scan(hist, G, hist + G);
       const uint32_t w = sh[2];
       if (c0 == 0) tmark(10, true);
       const size_t b64 = (size_t)w * CH * ASZ;
@@ -218,11 +272,11 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
           stage[hist[fb & (G - 1)] + rk[s]] =
               (unsigned long long)u | ((unsigned long long)li << UB) | ((unsigned long long)acc[s] << (UB + LB));
         }
-      __syncthreads();
+      lds_barrier();
       if (c0 == 0) tmark(11, true);
       if (ok)
         for (uint32_t r = tid; r < total; r += PB_T) st_agent64(&area[b64 + r], stage[r]);
-      __syncthreads();  // (stage and hist are reused by the next chunk)
+      lds_barrier();  // (stage and hist are reused by the next chunk)
       if (c0 == 0) tmark(12, true);
     }
     tmark(1, true);
@@ -230,8 +284,9 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
     pb_grid_sync(p.blk, ++ep, G, a.err);
     tmark(2, true);
     // ---------------------------------------------- receive level L's records (hop L + 1) ----
-    const uint32_t ns = min(ld_agent32(&p.blk[256 + L]), p.rows_cap);  // (grid-uniform)
+    const uint32_t ns = min(ld_agent32(&p.blk[PB_SLICES + L]), p.rows_cap);  // (grid-uniform)
     if (ns == 0) break;
+    if (tid == 0) sh[3] = 0;  // touched nodes
     for (uint32_t c0 = 0; c0 < ns; c0 += PB_SEG) {
       const uint32_t gc = min(PB_SEG, ns - c0);
       for (uint32_t i = tid; i < gc; i += PB_T) {
@@ -239,13 +294,13 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
         pre[i] = ld_agent32(&T[(size_t)(2 + g) * p.TS + c0 + i]) - st;  // (row 1 + G: the run's total)
         sb[i] = ld_agent32(&T[c0 + i]) + st;
       }
-      __syncthreads();
+      lds_barrier();
       if (c0 == 0) tmark(13, true);
-      const uint32_t ct = mv_block_scan(pre, gc, hist + G);
+      const uint32_t ct = pb_block_scan(pre, gc, hist + G);
       if (ct == 0) continue;  // (uniform)
-      if (trc && L < 120) atomicAdd(&p.tr[16 * L + 6], (unsigned long long)ct);
+      if (trc && L < PB_TRL) trl[16 * L + 6] += ct;
       if (tid == 0) pre[gc] = ct;
-      __syncthreads();
+      lds_barrier();
       if (c0 == 0) tmark(14, true);
       constexpr uint32_t AR = 4;  // records per thread per trip: searches and loads issued together
       for (uint32_t r0 = 0; r0 < ct; r0 += PB_T * AR) {
@@ -266,25 +321,29 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
           uint32_t li = (uint32_t)((rec[k] >> UB) & LBm);
           if (GS_OOB(li, NO, a.err, "pbfs record node")) li = 0;
           const uint32_t m = (uint32_t)(rec[k] >> (UB + LB));
-          atomicOr(&visL[li], m);
+          const uint32_t old = atomicOr(&visL[li], m);
+          // first arrivals: the node's first new bits of this level put it on the touched list once
+          if ((m & ~old) && !(old & ~visP[li])) tl[atomicAdd(&sh[3], 1u)] = li;
           const uint32_t lf = li >> BSF;
           const uint32_t pp = atomicAdd(&fcur[lf], 1u);
           if (pp < a.pcap)
             a.pool[(size_t)((lf << GL) + g) * a.pcap + pp] = mv_pool_rec(a, (uint32_t)(rec[k] & UBm), li & BPm, L + 1, m);
         }
       }
-      __syncthreads();
+      lds_barrier();  // (pre / sb are rewritten by the next batch)
     }
+    lds_barrier();
     tmark(3, true);
     // ---------------------------------------------- level L + 1 entries ----
+    const uint32_t nt = sh[3];
     uint32_t cntp = 0;
-    for (uint32_t i = tid; i < NO; i += PB_T) {
-      const uint32_t nw = visL[i] & ~visP[i];
-      if (nw) cntp += mv_parts(gt, node_of(i), nw, bk[i], nullptr, 0);
+    for (uint32_t k = tid; k < nt; k += PB_T) {
+      const uint32_t li = tl[k];
+      cntp += mv_parts(gt, node_of(li), visL[li] & ~visP[li], bk[li], nullptr, 0);
     }
     const uint32_t incl = wave_incl_scan(cntp);
     if ((tid & 63) == 63) hist[tid >> 6] = incl;
-    __syncthreads();
+    lds_barrier();
     uint32_t off = 0, tnew = 0;
     for (uint32_t k = 0; k < PB_T / 64; ++k) {
       if (k < (tid >> 6)) off += hist[k];
@@ -295,17 +354,19 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
       tnew = PB_EC + p.gq_cap;
     }
     uint32_t pos = off + incl - cntp;
-    for (uint32_t i = tid; i < NO; i += PB_T) {
-      const uint32_t nw = visL[i] & ~visP[i];
-      if (!nw) continue;
-      visP[i] = visL[i];
-      pos += mv_parts_to(gt, node_of(i), nw, bk[i], [&](uint32_t k, uint2 x) {
-        const uint32_t q = pos + k;
+    for (uint32_t k = tid; k < nt; k += PB_T) {
+      const uint32_t li = tl[k];
+      const uint32_t nw = visL[li] & ~visP[li];
+      visP[li] = visL[li];
+      pos += mv_parts_to(gt, node_of(li), nw, bk[li], [&](uint32_t j, uint2 x) {
+        const uint32_t q = pos + j;
         if (q < PB_EC) ent[q] = x;
-        else if (q < PB_EC + p.gq_cap) gq[q - PB_EC] = x;
+        else if (q < PB_EC + p.gq_cap) st_entry(&gq[q - PB_EC], x);
       });
     }
-    __syncthreads();  // (entries in LDS and in the workgroup's global region; hist is reused)
+    // entries in LDS; those in the workgroup's global region (sc1) are drained first
+    if (tnew > PB_EC) __syncthreads();
+    else lds_barrier();
     tmark(4, true);
     ++L;
     ne = tnew;
@@ -314,6 +375,13 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
       break;
     }
   }
+  if (trc)
+    for (uint32_t i = 0; i < PB_TRL * 16; ++i) {
+      const uint32_t k = i & 15;
+      if (k == 5 || k == 6) atomicAdd(&p.tr[i], (unsigned long long)trl[i]);
+      else if (k == 0) { if (g == 0) p.tr[i] = trl[i]; }
+      else atomicMax(&p.tr[i], (unsigned long long)trl[i]);
+    }
   // the pool fills of this workgroup's fine bins (k_mv_gather reads them)
   for (uint32_t lf = tid; lf < FPW; lf += PB_T) {
     const uint32_t fb = (lf << GL) + g;
@@ -333,13 +401,13 @@ static uint32_t ilog2(uint32_t x) {
 }  // namespace
 
 // LDS bytes of the persistent BFS workgroup (dynamic part).
-static size_t pb_stage_bytes(uint32_t stage_cap) {
-  const size_t stage = std::max<size_t>((size_t)stage_cap * 8, (2 * (size_t)PB_SEG + 1) * 4);
+static size_t pb_stage_bytes(uint32_t stage_cap, uint32_t NO) {
+  const size_t stage = std::max<size_t>((size_t)stage_cap * 8, (2 * (size_t)PB_SEG + 4 + NO) * 4);
   return (stage + 15) & ~(size_t)15;
 }
 static size_t pb_lds_bytes(uint32_t stage_cap, uint32_t NO, uint32_t G, uint32_t FPW) {
-  return PB_HDR + pb_stage_bytes(stage_cap) + 8 * (size_t)NO + 4 * ((size_t)G + 16) + 4 * (size_t)((FPW + 3) & ~3u) +
-         8 * (size_t)PB_EC + (size_t)NO;
+  return PB_HDR + pb_stage_bytes(stage_cap, NO) + 8 * (size_t)NO + 4 * ((size_t)G + 16) + 4 * (size_t)((FPW + 3) & ~3u) +
+         8 * (size_t)PB_EC + (((size_t)NO + 15) & ~(size_t)15) + 40 * 16 * 4;  // (+ the GS_PB_TRACE table)
 }
 
 // Process-wide count of engines that may launch the persistent BFS: two persistent
@@ -402,7 +470,7 @@ hipError_t launch_bfs_pers(Engine& e, const MvArgs& a, const MvGroup& gr) {
   p.seeds = e.mv_seed + gr.seed0;
   p.nseed = gr.nseed;
   p.G = e.pb_G; p.GL = e.pb_GL; p.FPW = e.pb_FPW; p.LB = e.pb_LB; p.CH = e.pb_CH;
-  p.stage_bytes = (uint32_t)pb_stage_bytes(e.pb_CH * e.ASZ);
+  p.stage_bytes = (uint32_t)pb_stage_bytes(e.pb_CH * e.ASZ, e.pb_FPW << e.mv.BSF);
   p.rows_cap = e.pb_rows_cap; p.TS = e.pb_rows_cap;
   p.T[0] = e.pb_T[0]; p.T[1] = e.pb_T[1];
   p.area[0] = e.pb_area[0]; p.area[1] = e.pb_area[1];
@@ -415,7 +483,7 @@ hipError_t launch_bfs_pers(Engine& e, const MvArgs& a, const MvGroup& gr) {
     return x ? std::atoi(x) : 0;
   }();
   static unsigned long long* trd = nullptr;
-  static unsigned long long trh[1920];
+  static unsigned long long trh[640];
   static int launches = 0;
   const bool trace = trace_launch > 0 && ++launches == trace_launch;
   if (trace) {  // (device memory: the kernel's atomics on it stay on the device)
@@ -424,17 +492,24 @@ hipError_t launch_bfs_pers(Engine& e, const MvArgs& a, const MvGroup& gr) {
     p.tr = trd;
   }
   if ((r = hipMemsetAsync(e.pb_blk, 0, PB_BLK_WORDS * 4, e.st))) return r;
+  static const bool twice = std::getenv("GS_PB_TWICE") && std::getenv("GS_PB_TWICE")[0] == '1';  // (diagnostics)
+  if (twice) {
+    PbArgs q = p;
+    q.tr = nullptr;
+    GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_pbfs<A>), dim3(e.pb_G), dim3(PB_T), e.pb_lds, e.st, q));
+    if ((r = hipMemsetAsync(e.pb_blk, 0, PB_BLK_WORDS * 4, e.st))) return r;
+  }
   GS_ASZP_DISPATCH(e.ASZP, hipLaunchKernelGGL((k_mv_pbfs<A>), dim3(e.pb_G), dim3(PB_T), e.pb_lds, e.st, p));
   if (trace) {  // (diagnostics: waits for the launch; clocks at 100 MHz)
     if ((r = hipMemcpyAsync(trh, trd, sizeof(trh), hipMemcpyDeviceToHost, e.st)) || (r = hipStreamSynchronize(e.st)))
       return r;
     std::fprintf(stderr, "GS_PB_TRACE launch %d: level, start us, max expand / barrier / receive / entries us, entries, "
-                 "records | expand: clear, entries+rank, scan+slice, T+stage, area | receive: T column, scan\n", launches);
-    for (int L = 0; L < 120 && (L == 0 || trh[16 * L + 5] || trh[16 * L + 6]); ++L) {
+                 "records | expand: clear, entries+rank, scan+slice, T+stage, area, (thread 0's entry) | receive: T column, scan\n", launches);
+    for (int L = 0; L < 40 && (L == 0 || trh[16 * L + 5] || trh[16 * L + 6]); ++L) {
       const unsigned long long* t = trh + 16 * L;
-      std::fprintf(stderr, "  %3d %8.1f %6.1f %6.1f %6.1f %6.1f %8llu %8llu | %5.1f %5.1f %5.1f %5.1f %5.1f | %5.1f %5.1f\n", L,
-                   t[0] / 100.0, t[1] / 100.0, t[2] / 100.0, t[3] / 100.0, t[4] / 100.0, t[5], t[6], t[8] / 100.0,
-                   t[9] / 100.0, t[10] / 100.0, t[11] / 100.0, t[12] / 100.0, t[13] / 100.0, t[14] / 100.0);
+      std::fprintf(stderr, "  %3d %8.1f %6.1f %6.1f %6.1f %6.1f %8llu %8llu | %5.1f %5.1f %5.1f %5.1f %5.1f (%5.1f) | %5.1f %5.1f\n",
+                   L, t[0] / 100.0, t[1] / 100.0, t[2] / 100.0, t[3] / 100.0, t[4] / 100.0, t[5], t[6], t[8] / 100.0,
+                   t[9] / 100.0, t[10] / 100.0, t[11] / 100.0, t[12] / 100.0, t[7] / 100.0, t[13] / 100.0, t[14] / 100.0);
     }
   }
   return hipGetLastError();

@@ -10,4 +10,4 @@ if [ -n "${TESTS:-}" ]; then
   rc=$?; tail -5 $OUT/gpu_tests.log
   if [ $rc -ne 0 ]; then grep -E "FAILED|Error|error|assert" $OUT/gpu_tests.log | head -30; exit $rc; fi
 fi
-TAG=${TAG:-quick} scripts/r06_iter.sh
+TESTS= TAG=${TAG:-quick} scripts/r06_iter.sh
