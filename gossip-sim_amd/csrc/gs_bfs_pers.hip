@@ -149,6 +149,71 @@ __device__ inline uint2 ld_entry(const uint2* p) {
   return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
 }
 
+// One frontier entry per LW lanes (lane j of the group: slot j), for a workgroup's levels of
+// at most PB_T / LW entries: the slots' selections run side by side instead of one after
+// another in one lane (a 13-slot entry was a ~6-9 us VALU chain of one lane, and C4's first
+// levels hold 1-36 entries per workgroup). Per slot the selection of mv_expand_entry:
+// taken_slots (push_active_set.rs:128-141: the first `fanout` unpruned non-origin ring
+// slots in FIFO order), then failed peers burn their slot (gossip.rs:527-541); the slot's
+// egress byte. Lane j < ASZP returns ring slot j's record (its peer and the slots that push
+// to it) in row[0] / acc[0].
+template <int ASZP, uint32_t LW>
+__device__ inline void pb_expand_wide(const MvArgs& a, uint2 ent, bool valid, const MvSlots& S, uint32_t (&row)[ASZP],
+                                      uint32_t (&acc)[ASZP], uint32_t& u) {
+  constexpr int TQ = (mv_orw<ASZP>() - ASZP) / 4;
+  const uint32_t lane = threadIdx.x & 63, j = lane & (LW - 1), gb = lane & ~(LW - 1);
+  u = ent.x & 0xFFFFFFu;
+  const uint32_t k = ent.x >> 24, M = valid ? ent.y : 0u;
+  if (GS_OOB(u, a.N, a.err, "pbfs wide node")) u = 0;
+  const bool inM = (M >> j) & 1u;
+  uint32_t rw[ASZP];
+  const uint32_t* orow = a.own + (size_t)u * a.ORW;
+  load_row<ASZP>(orow, rw);
+  uint32_t tail[4 * TQ];
+  {
+    const uint4* t4 = reinterpret_cast<const uint4*>(orow + ASZP);
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) {
+      const uint4 x = t4[q];
+      tail[4 * q] = x.x; tail[4 * q + 1] = x.y; tail[4 * q + 2] = x.z; tail[4 * q + 3] = x.w;
+    }
+  }
+  const uint32_t pm = inM ? a.mask[(size_t)u * a.MSU + a.s0 + j] : 0u;
+  uint32_t hv = tail[0] & 0xFFFFu, fc[ASZP];
+  if ((tail[0] >> 16) == k) {
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) fc[s] = (tail[1 + s / 4] >> (8 * (s % 4))) & 0xFFu;
+  } else {  // an origin of lower bucket: entry min(bucket[u], bucket[origin])
+    const uint32_t ent_i = u * NB + k;
+    hv = a.hl[ent_i];
+    load_row<ASZP>(a.peers + (size_t)ent_i * ASZP, rw);
+#pragma unroll
+    for (int s = 0; s < ASZP; ++s) fc[s] = a.any_fail ? a.fcls[rw[s]] : 0xFFu;
+  }
+  uint32_t tk = 0;
+  if (inM) {
+    tk = taken_slots<ASZP>(rw, hv & 0xFF, hv >> 8, a.ASZ, pm, S.sorg[j], a.fanout);
+    const uint32_t f = S.sfk[j];
+    if (f) {  // failed peers burn their fanout slot (gossip.rs:538-541)
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s)
+        if (fc[s] <= f) tk &= ~(1u << s);
+    }
+    if (u - a.vlo < a.vhi - a.vlo) a.egress[(size_t)(u - a.vlo) * a.SP + a.s0 + j] = (uint8_t)__popc(tk);
+  }
+  uint32_t mr = 0, ma = 0;
+#pragma unroll
+  for (int s = 0; s < ASZP; ++s) {
+    const uint64_t b = __ballot((tk >> s) & 1u);
+    const uint32_t m = (uint32_t)(b >> gb) & (LW == 32 ? 0xFFFFFFFFu : 0xFFFFu);
+    if (j == (uint32_t)s) { ma = m; mr = rw[s]; }
+  }
+#pragma unroll
+  for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
+  row[0] = mr;
+  acc[0] = ma;
+}
+
 template <int ASZP>
 __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -219,6 +284,8 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
     const unsigned long long now = wall_clock64();
     if (mx) trl[16 * L + slot] = max(trl[16 * L + slot], (uint32_t)(now - tm));
     else trl[16 * L + slot] = (uint32_t)(now - t0);
+    if (slot == 1) trl[16 * L + 15] += (uint32_t)(now - tm);  // (sums over workgroups: expand, receive)
+    if (slot == 3) trl[16 * L + 14] += (uint32_t)(now - tm);
     tm = now;
   };
   for (;;) {
@@ -228,7 +295,11 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
     const uint32_t par = L & 1;
     uint32_t* T = p.T[par];
     unsigned long long* area = p.area[par];
-    for (uint32_t c0 = 0; c0 < ne; c0 += CH) {  // (ne is workgroup-uniform)
+    // few entries: one entry per LW lanes, in one chunk (pb_expand_wide)
+    constexpr uint32_t LW = ASZP <= 16 ? 16u : 32u;
+    const bool wide = a.Sg <= LW && ne <= PB_T / LW;
+    const uint32_t step = wide ? PB_T / LW : CH;
+    for (uint32_t c0 = 0; c0 < ne; c0 += step) {  // (ne is workgroup-uniform)
       // the chunk's slice: the returned value is first needed after the expansion (its
       // latency overlaps the row loads)
       uint32_t wsl = 0;
@@ -240,7 +311,12 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
       const uint32_t i = c0 + tid;
-      if (tid < CH && i < ne) mv_expand_entry<ASZP>(a, i < PB_EC ? ent[i] : ld_entry(&gq[i - PB_EC]), S, row, acc, u);
+      if (wide) {
+        const uint32_t e = tid / LW;
+        pb_expand_wide<ASZP, LW>(a, e < ne ? ent[e] : make_uint2(0u, 0u), e < ne, S, row, acc, u);
+      } else if (tid < CH && i < ne) {
+        mv_expand_entry<ASZP>(a, i < PB_EC ? ent[i] : ld_entry(&gq[i - PB_EC]), S, row, acc, u);
+      }
       if (trc && c0 == 0) {  // (trace: thread 0's own entry, its loads and stores drained)
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         tmark(7, true);
@@ -301,7 +377,7 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
       if (trc && L < PB_TRL) trl[16 * L + 6] += ct;
       if (tid == 0) pre[gc] = ct;
       lds_barrier();
-      if (c0 == 0) tmark(14, true);
+      if (c0 == 0) tmark(13, true);
       constexpr uint32_t AR = 4;  // records per thread per trip: searches and loads issued together
       for (uint32_t r0 = 0; r0 < ct; r0 += PB_T * AR) {
         unsigned long long rec[AR];
@@ -378,7 +454,7 @@ __global__ __launch_bounds__(PB_T, 1) void k_mv_pbfs(PbArgs p) {
   if (trc)
     for (uint32_t i = 0; i < PB_TRL * 16; ++i) {
       const uint32_t k = i & 15;
-      if (k == 5 || k == 6) atomicAdd(&p.tr[i], (unsigned long long)trl[i]);
+      if (k == 5 || k == 6 || k == 14 || k == 15) atomicAdd(&p.tr[i], (unsigned long long)trl[i]);
       else if (k == 0) { if (g == 0) p.tr[i] = trl[i]; }
       else atomicMax(&p.tr[i], (unsigned long long)trl[i]);
     }
@@ -504,12 +580,14 @@ hipError_t launch_bfs_pers(Engine& e, const MvArgs& a, const MvGroup& gr) {
     if ((r = hipMemcpyAsync(trh, trd, sizeof(trh), hipMemcpyDeviceToHost, e.st)) || (r = hipStreamSynchronize(e.st)))
       return r;
     std::fprintf(stderr, "GS_PB_TRACE launch %d: level, start us, max expand / barrier / receive / entries us, entries, "
-                 "records | expand: clear, entries+rank, scan+slice, T+stage, area, (thread 0's entry) | receive: T column, scan\n", launches);
+                 "records | expand: clear, entries+rank, scan+slice, T+stage, area, (thread 0's entry) | receive: T column+scan | "
+                 "mean expand, receive\n", launches);
     for (int L = 0; L < 40 && (L == 0 || trh[16 * L + 5] || trh[16 * L + 6]); ++L) {
       const unsigned long long* t = trh + 16 * L;
-      std::fprintf(stderr, "  %3d %8.1f %6.1f %6.1f %6.1f %6.1f %8llu %8llu | %5.1f %5.1f %5.1f %5.1f %5.1f (%5.1f) | %5.1f %5.1f\n",
+      std::fprintf(stderr, "  %3d %8.1f %6.1f %6.1f %6.1f %6.1f %8llu %8llu | %5.1f %5.1f %5.1f %5.1f %5.1f (%5.1f) | %5.1f | %5.1f %5.1f\n",
                    L, t[0] / 100.0, t[1] / 100.0, t[2] / 100.0, t[3] / 100.0, t[4] / 100.0, t[5], t[6], t[8] / 100.0,
-                   t[9] / 100.0, t[10] / 100.0, t[11] / 100.0, t[12] / 100.0, t[7] / 100.0, t[13] / 100.0, t[14] / 100.0);
+                   t[9] / 100.0, t[10] / 100.0, t[11] / 100.0, t[12] / 100.0, t[7] / 100.0, t[13] / 100.0,
+                   t[15] / 100.0 / e.pb_G, t[14] / 100.0 / e.pb_G);
     }
   }
   return hipGetLastError();

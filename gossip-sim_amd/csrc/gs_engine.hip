@@ -81,6 +81,7 @@ static int dalloc(Engine& e, T** p, size_t count, int fill = 0) {
   } while (0)
 
 static int flush_rot_clear(Engine* e);
+static int ensure_rot_ahead(Engine* e);
 
 template <class T>
 static void dfree(Engine& e, T*& p, size_t count) {
@@ -348,7 +349,8 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
   e->fused = mode == GS_BFS_WORKGROUP && !(prm->flags & GS_FLAG_SPLIT_ROUND) &&
              round_wg_lds_bytes(n, e->fcap, e->ASZP) <= 160 * 1024;
   // rotation ahead of the fused round (one-workgroup rotation sizes; GS_ROT_AHEAD=0: off)
-  e->rot_ahead_ok = e->fused && n <= 16384 && !(std::getenv("GS_ROT_AHEAD") && std::getenv("GS_ROT_AHEAD")[0] == '0');
+  e->rot_ahead_ok = e->fused && n <= 16384 && round_wg_lds_bytes(n, e->fcap, e->ASZP) >= 4 * ((size_t)n + 1) &&
+                    !(std::getenv("GS_ROT_AHEAD") && std::getenv("GS_ROT_AHEAD")[0] == '0');
 
   const size_t N = n, S = n_slots, PAIRS = e->PAIRS, NP = e->NP;
   e->SP = (uint32_t)((S + 3) & ~(size_t)3);
@@ -513,6 +515,9 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
     }
   }
   if (const char* pp = std::getenv("GS_PHASE_PROFILE"); pp && pp[0] == '1') ALLOC(e->phase_clk, 32, 0);
+  if (e->rot_ahead_ok) {  // the rotation-ahead buffers at create: counted in the engine's memory, fail here
+    if (int s_ = ensure_rot_ahead(e)) { destroy_engine(e); return s_; }
+  }
 
   // stakes, buckets and the static rotation prefix sums
   std::vector<uint8_t> b(N);
@@ -617,6 +622,10 @@ int gs_set_slots(gs_engine* eh, const gs_slot* slots, uint32_t n_slots) {
     mi[o] = slots[o].min_ingress_nodes;
     thr[o] = slots[o].prune_stake_threshold;
   }
+  // from the first upload on, the device holds a mix of old and new slot state until this
+  // call returns GS_OK: any failure below leaves the engine without slots (every BFS call
+  // is refused until set_slots succeeds)
+  e->slots_set = false;
   HIPC(hipMemcpyAsync(e->origin, org.data(), e->S * 4, hipMemcpyHostToDevice, e->st));
   HIPC(hipMemcpyAsync(e->obkt, ob.data(), e->S, hipMemcpyHostToDevice, e->st));
   HIPC(hipMemcpyAsync(e->min_ingress, mi.data(), e->S * 4, hipMemcpyHostToDevice, e->st));
@@ -854,13 +863,24 @@ int gs_record_round(gs_engine* eh) {
 // in workgroup 0 of the round kernel into the other row buffer, concurrently with the
 // slots' workgroups on the current one, and the buffers swap after the launch (no rotation
 // launch, nothing between two round kernels).
+// The second row buffer and the alternate rotation list / changed-bit buffers. All four
+// or none: a failed allocation frees the ones made, so a retried call allocates again
+// (a partial set left peers2 set and a later round wrote through a null hl2).
 static int ensure_rot_ahead(Engine* e) {
-  if (e->peers2) return GS_OK;
+  if (e->peers2 && e->hl2 && e->rot_list_b[1] && e->rot_changed_b[1]) return GS_OK;
   const size_t N = e->N;
-  if (int s = dalloc(*e, &e->peers2, N * NB * e->ASZP, 0)) return s;
-  if (int s = dalloc(*e, &e->hl2, N * NB, 0)) return s;
-  if (int s = dalloc(*e, &e->rot_list_b[1], N, 0)) return s;
-  if (int s = dalloc(*e, &e->rot_changed_b[1], N * NB, 0)) return s;
+  int s = GS_OK;
+  if (!e->peers2) s = dalloc(*e, &e->peers2, N * NB * e->ASZP, 0);
+  if (!s && !e->hl2) s = dalloc(*e, &e->hl2, N * NB, 0);
+  if (!s && !e->rot_list_b[1]) s = dalloc(*e, &e->rot_list_b[1], N, 0);
+  if (!s && !e->rot_changed_b[1]) s = dalloc(*e, &e->rot_changed_b[1], N * NB, 0);
+  if (s) {
+    dfree(*e, e->peers2, N * NB * e->ASZP);
+    dfree(*e, e->hl2, N * NB);
+    dfree(*e, e->rot_list_b[1], N);
+    dfree(*e, e->rot_changed_b[1], N * NB);
+    return s;
+  }
   e->rot_list_b[0] = e->rot_list;
   e->rot_changed_b[0] = e->rot_changed;
   e->rows2_stale = true;

@@ -176,7 +176,9 @@ struct Engine {
   // (seed, node, round) and the rows, not on the round's BFS or prunes -- and the buffers
   // swap after the round. rot_list / rot_changed alternate between two buffers so the
   // round kernel's deferred clear of the previous rotation is not overwritten.
-  bool rot_ahead_ok = false;        // enabled at create; off for good once a step API runs
+  bool rot_ahead_ok = false;        // enabled at create (its buffers allocated there); stays on: any
+                                    // in-place row change (init, a step-wise rotation, an uploaded
+                                    // entry) must set rows2_stale (a full copy before the next round)
   bool rows2_stale = true;          // peers2 / hl2 need a full copy of peers / hl
   bool rot_cnt_dirty = false;       // an ahead rotation did not zero the other counter
   int rows2_pending = -1;           // parity of the rotation applied to peers but not peers2

@@ -127,12 +127,15 @@ constexpr uint32_t MV_SG4 = 7;  // slot quads per group (GW <= 28)
 __host__ __device__ inline uint32_t mv_ohash(uint32_t x) { return (x * 0x9E3779B1u) >> 25; }
 
 // The group's slots as the expand reads them (LDS): origins, failure classes, the slots
-// with no failures (fz; 0 when the origin hash is incomplete, so that every slot takes
-// the per-slot path), and the origin -> slot-mask hash of the group table.
+// that may take the shared-prefix path (pz: all, or none when the origin hash is
+// incomplete, so that every slot takes the per-slot path), the origin -> slot-mask hash of
+// the group table, and per failure class c the slots in which a peer of class c failed
+// (fm[c] = slots j with 0 < c <= fk[j]; class 255 = fails nowhere, fm[255] = 0).
 struct MvSlots {
   uint32_t sorg[32], sfk[32];
   uint2 otab[128];
-  uint32_t fz;
+  uint32_t fm[256];
+  uint32_t pz;
 };
 
 // (no barrier: the caller's first __syncthreads publishes S)
@@ -143,10 +146,16 @@ __device__ inline void mv_slots_load(const MvArgs& a, MvSlots& S, uint32_t tid, 
   }
   const uint2* ot = reinterpret_cast<const uint2*>(a.gt + GT_OT);
   for (uint32_t i = tid; i < 128; i += nth) S.otab[i] = ot[i];
-  if (tid < 64) {  // wave 0 (every kernel has >= 256 threads)
-    const uint64_t z = __ballot(tid < a.Sg && a.fk[a.s0 + tid] == 0);
-    if (tid == 0) S.fz = a.gt[GT_OTOK] ? (uint32_t)z : 0u;
+  for (uint32_t c = tid; c < 256; c += nth) {
+    uint32_t m = 0;
+    if (a.any_fail && c != 0)
+      for (uint32_t j = 0; j < a.Sg; ++j) {
+        const uint32_t f = a.fk[a.s0 + j];
+        m |= (uint32_t)(f != 0 && c <= f) << j;
+      }
+    S.fm[c] = m;
   }
+  if (tid == 0) S.pz = a.gt[GT_OTOK] ? 0xFFFFFFFFu : 0u;
 }
 
 // The group's slots whose origin is node x.
@@ -165,12 +174,15 @@ constexpr int mv_orw() { return ((ASZP + 1 + ASZP / 4) + 3) & ~3; }
 // slot in M (PushActiveSet::get_nodes(..).take(fanout), gossip.rs:527-541: unpruned,
 // not the origin, failed peers burn their slot) as per-ring-slot slot masks acc[s], and
 // each slot's egress byte.
-// Plain slots (no prunes at u, no failures) push to the first `fanout` ring positions
-// except their own origin: one prefix of the ring for all of them, and a slot whose
-// origin sits in that prefix swaps it for position `fanout` (the group's origins are
-// looked up once per pushed-to peer in an LDS hash). Only the other slots run the
-// per-slot selection, which a wave executes for the union of its lanes' slots (round 4;
-// before, every slot of M ran it unless it shared the group's first origin).
+// Plain slots (no prunes at u) push to the first `fanout` ring positions except their
+// own origin: one prefix of the ring for all of them, and a slot whose origin sits in that
+// prefix swaps it for position `fanout` (the group's origins are looked up once per
+// pushed-to peer in an LDS hash). Failed peers burn their slot (the take(fanout) comes
+// before the failed check), so a plain slot's failures only remove pushes from the prefix:
+// ring slot s loses the slots fm[class of its peer] (round 6; before, every slot with
+// failures ran the per-slot selection -- C4's five fail-nodes slots at every entry). Only
+// slots with prune bits at u run the per-slot selection, which a wave executes for the
+// union of its lanes' slots. Plain slots' push counts come from bit-sliced counters.
 template <int ASZP, bool EG = true>  // EG: write the egress bytes of the entry's slots
 __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const MvSlots& S, uint32_t (&row)[ASZP],
                                        uint32_t (&acc)[ASZP], uint32_t& u) {
@@ -208,14 +220,14 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const MvSlots
     for (int s = 0; s < ASZP; ++s) fc[s] = a.any_fail ? a.fcls[row[s]] : 0xFFu;
   }
   const uint32_t head = hv & 0xFF, len = hv >> 8;
-  uint32_t plain = 0, ep = 0, epr = 0;
+  uint32_t plain = 0, pc0 = 0, pc1 = 0, pc2 = 0, pc3 = 0, pc4 = 0;  // (plain slots' push counts, bit-sliced)
   if constexpr (ASZP < 32) {
     uint32_t pmz = 0;  // slots with no prunes at u
 #pragma unroll
     for (uint32_t q = 0; q < MV_SG4; ++q)
       pmz |= ((uint32_t)(m4[q].x == 0) | ((uint32_t)(m4[q].y == 0) << 1) | ((uint32_t)(m4[q].z == 0) << 2) |
               ((uint32_t)(m4[q].w == 0) << 3)) << (4 * q);
-    plain = M & S.fz & pmz;
+    plain = M & S.pz & pmz;
     if (plain) {
       const uint32_t SZ = a.ASZ, full = (1u << SZ) - 1u;
       const uint32_t L = min(len, SZ), nf = min(L, a.fanout);
@@ -223,20 +235,31 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const MvSlots
       const uint32_t tkn = ((pre << head) | (pre >> (SZ - head))) & full;               // physical slots
       const uint32_t nxt = ((nxp << head) | (nxp >> (SZ - head))) & full;
       uint32_t rem = 0;  // plain slots whose origin is in the prefix
+      uint32_t ap[ASZP];
 #pragma unroll
       for (int s = 0; s < ASZP; ++s) {
+        ap[s] = 0;
         if (!((tkn >> s) & 1u)) continue;
         const uint32_t om = mv_origin_slots(S, row[s]) & plain;
-        acc[s] |= plain & ~om;
+        ap[s] = plain & ~om;
         rem |= om;
       }
       if (rem) {
 #pragma unroll
         for (int s = 0; s < ASZP; ++s)
-          if ((nxt >> s) & 1u) acc[s] |= rem;
+          if ((nxt >> s) & 1u) ap[s] |= rem;
       }
-      ep = (uint32_t)__popc(tkn);
-      epr = nxt ? 0u : rem;  // (no position `fanout`: those slots push one fewer)
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        if (a.any_fail && ap[s]) ap[s] &= ~S.fm[fc[s]];  // failed peers burn their slot (gossip.rs:538-541)
+        acc[s] |= ap[s];
+        uint32_t x = ap[s], t;  // bit-sliced add: pushes per plain slot (<= fanout < 32)
+        t = pc0 & x; pc0 ^= x; x = t;
+        t = pc1 & x; pc1 ^= x; x = t;
+        t = pc2 & x; pc2 ^= x; x = t;
+        t = pc3 & x; pc3 ^= x; x = t;
+        pc4 ^= x;
+      }
     }
   }
   const bool own_u = u - a.vlo < a.vhi - a.vlo;  // egress is kept for owned nodes
@@ -252,7 +275,8 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const MvSlots
       const uint32_t j = 4 * q + t;
       if (!((mq4 >> t) & 1u)) continue;
       if ((plain >> j) & 1u) {
-        egw |= (ep - ((epr >> j) & 1u)) << (8 * t);
+        egw |= (((pc0 >> j) & 1u) | (((pc1 >> j) & 1u) << 1) | (((pc2 >> j) & 1u) << 2) | (((pc3 >> j) & 1u) << 3) |
+                (((pc4 >> j) & 1u) << 4)) << (8 * t);
         continue;
       }
       const uint32_t pm = t == 0 ? m4[q].x : t == 1 ? m4[q].y : t == 2 ? m4[q].z : m4[q].w;

@@ -634,10 +634,12 @@ __device__ inline void compact_push(const uint32_t (&row)[ASZP], uint32_t pushm,
 // current rows), then this round's rotation (decide, gossip.rs:739-754; rotate_entry,
 // push_active_set.rs:73-114,153-187) on the other buffer. The slots' workgroups only read
 // the current buffer, so the two never touch the same rows.
+// lids: the workgroup's dynamic LDS, N node ids and the count after them (the create-time
+// gate checks 4 (N + 1) bytes fit: no static LDS beside the round's layout)
 template <int ASZP>
 __device__ void rotate_ahead_wg(const RoundArgs& a, uint32_t* lids) {
-  __shared__ uint32_t lcount;
   const uint32_t tid = threadIdx.x, T = blockDim.x, N = a.N;
+  uint32_t& lcount = lids[N];
   if (a.plist) {
     const uint32_t total = *a.pcount * NB;
     for (uint32_t gid = tid; gid < total; gid += T) {
