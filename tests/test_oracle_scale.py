@@ -290,6 +290,7 @@ def sweep_vs_oracle(n, slots, mode, env, monkeypatch, rounds=22, p=0.0, full_eve
 
     with ThreadPoolExecutor(max_workers=S) as ex:
         for r in range(rounds):
+            print(f"sweep_vs_oracle n={n} slots={S} p={p}: round {r}", flush=True)  # (progress, pytest -s)
             full = r % full_every == 0 or 18 <= r <= 20 or r == rounds - 1
             futs = [ex.submit(oracle_round, k, r, full) for k in range(S)]
             eng.round(r, record=True)

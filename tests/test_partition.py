@@ -124,7 +124,13 @@ def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend, exchang
     if case == "large" and exchange == "auto" and bfs == "replicated":
         # device memory per rank: its share of the per-(slot, node) state + the replicated tables
         # (the forced-records run enlarges the record buffer by GS_PART_RECORD_CAP: not compared)
-        full = eb.gs.Engine(st, S, bfs_mode=eb.gs.GS_BFS_MULTI, seed=c["seed"], rotation_probability=c["p"])
+        # (the reference engine without the persistent BFS's level buffers: a partition rank
+        # runs the launched level loop and allocates none)
+        os.environ["GS_MV_PBFS"] = "0"
+        try:
+            full = eb.gs.Engine(st, S, bfs_mode=eb.gs.GS_BFS_MULTI, seed=c["seed"], rotation_probability=c["p"])
+        finally:
+            os.environ.pop("GS_MV_PBFS", None)
         fi = full.info()
         full.close()
         for p in parts:
