@@ -94,6 +94,11 @@ EXPORTS = {
     "gs_part_xbfs_apply": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int,
                                      C.POINTER(C.c_uint32)]),
     "gs_part_xbfs_end": (C.c_int, [C.c_void_p, C.c_int]),
+    "gs_part_xbfs_expand_async": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p]),
+    "gs_part_xbfs_apply_async": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
+    "gs_part_xbfs_async_status": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_void_p,
+                                            C.c_size_t]),
+    "gs_stream": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "gs_part_xround_finish": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.POINTER(C.c_uint32)]),
     "gs_part_stats_out": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "gs_part_stats_in": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),

@@ -1069,9 +1069,15 @@ __global__ __launch_bounds__(MV_GT) __attribute__((amdgpu_waves_per_eu(4))) void
 // entries). Ranks own whole coarse bins, so a bin's records go to one rank.
 
 // Records per coarse bin in level d's G expand runs (the T column of bin c).
-__global__ __launch_bounds__(256) void k_mvx_bincount(MvArgs a, uint32_t G, uint32_t* __restrict__ bincnt) {
+// (G = ~0: level d's slices, from its size on the device -- the asynchronous level loop)
+__device__ inline uint32_t mvx_slices(const MvArgs& a, uint32_t G, uint32_t d) {
+  return G != 0xFFFFFFFFu ? G : min((a.lvl[d] + a.XT - 1) / a.XT, (uint32_t)a.rows_cap);
+}
+
+__global__ __launch_bounds__(256) void k_mvx_bincount(MvArgs a, uint32_t G, uint32_t d, uint32_t* __restrict__ bincnt) {
   __shared__ uint32_t part[4];
   const uint32_t c = blockIdx.x;
+  G = mvx_slices(a, G, d);
   uint32_t s = 0;
   for (uint32_t i = threadIdx.x; i < G; i += 256) {
     s += mv_t(a, i, 2 + c) - mv_t(a, i, 1 + c);
@@ -1085,13 +1091,18 @@ __global__ __launch_bounds__(256) void k_mvx_bincount(MvArgs a, uint32_t G, uint
 
 // Bin c's segments of the G expand runs, copied contiguously (slice order) to out[rpos[c]..],
 // and its record count to out[hpos[c]]: the header word of the owner's message.
-__global__ __launch_bounds__(256) void k_mvx_pack(MvArgs a, uint32_t G, const unsigned long long* __restrict__ hpos,
+// (rpos[c] = ~0: the owner's message outgrew its slot -- the header says 0 records)
+__global__ __launch_bounds__(256) void k_mvx_pack(MvArgs a, uint32_t G, uint32_t d,
+                                                  const unsigned long long* __restrict__ hpos,
                                                   const unsigned long long* __restrict__ rpos,
                                                   const uint32_t* __restrict__ bincnt,
                                                   unsigned long long* __restrict__ out) {
   __shared__ uint32_t pre[MV_SEG + 1], sb[MV_SEG], wsum[16];
   const uint32_t c = blockIdx.x, tid = threadIdx.x;
-  if (tid == 0) out[hpos[c]] = bincnt[c];
+  G = mvx_slices(a, G, d);
+  const bool skip = rpos[c] == ~0ull;
+  if (tid == 0) out[hpos[c]] = skip ? 0u : bincnt[c];
+  if (skip) return;
   size_t dst = rpos[c];
   for (uint32_t c0 = 0; c0 < G; c0 += MV_SEG) {
     const uint32_t gc = min(MV_SEG, G - c0);
@@ -1120,11 +1131,13 @@ __global__ __launch_bounds__(256) void k_mvx_pack(MvArgs a, uint32_t G, const un
 // T row q of a received level (bin-major with stride K, as mv_t): sender q's message (words
 // off[q] ..) is nbm header words (record counts of this rank's bins blo, blo + 1, ...) then the
 // records, bin by bin.
+// (off = null: sender q's message starts at q * cap, the asynchronous loop's fixed slots)
 __global__ __launch_bounds__(64) void k_mvx_trows(const unsigned long long* __restrict__ recv,
-                                                  const unsigned long long* __restrict__ off, uint32_t blo, uint32_t nbm,
-                                                  uint32_t nbc, uint32_t K, uint32_t* __restrict__ T) {
+                                                  const unsigned long long* __restrict__ off, unsigned long long cap,
+                                                  uint32_t blo, uint32_t nbm, uint32_t nbc, uint32_t K,
+                                                  uint32_t* __restrict__ T) {
   const uint32_t q = blockIdx.x;
-  const unsigned long long o = off[q];
+  const unsigned long long o = off ? off[q] : (unsigned long long)q * cap;
   for (uint32_t b = threadIdx.x; b < blo; b += 64) T[(size_t)(1 + b) * K + q] = 0;
   if (threadIdx.x == 0) {
     T[q] = (uint32_t)(o + nbm);
@@ -1134,6 +1147,32 @@ __global__ __launch_bounds__(64) void k_mvx_trows(const unsigned long long* __re
       run += (uint32_t)recv[o + i];
     }
     for (uint32_t b = blo + nbm; b <= nbc; ++b) T[(size_t)(1 + b) * K + q] = run;
+  }
+}
+
+// The asynchronous level loop's message layout (one thread per owner rank q): q's message
+// goes to the fixed slot [q * cap, (q + 1) * cap) of the send buffer -- its bins' counts, then
+// their records -- so no size has to reach the host before the all-to-all. xbin[2q], xbin[2q+1]:
+// q's first coarse bin and bin count; wlog[q]: the message's words (the next round's
+// capacity prediction). A message larger than its slot raises ERR_MVX_CAP and is sent as
+// counts of 0 (the group's BFS is then redone with exact sizes).
+__global__ void k_mvx_layout(uint32_t K, const uint32_t* __restrict__ xbin, const uint32_t* __restrict__ bincnt,
+                             unsigned long long cap, unsigned long long* __restrict__ hpos,
+                             unsigned long long* __restrict__ rpos, unsigned long long* __restrict__ wlog,
+                             uint32_t* __restrict__ err) {
+  for (uint32_t q = threadIdx.x; q < K; q += blockDim.x) {
+    const uint32_t f = xbin[2 * q], nb = xbin[2 * q + 1];
+    unsigned long long w = nb;
+    for (uint32_t i = 0; i < nb; ++i) w += bincnt[f + i];
+    wlog[q] = w;
+    const bool over = w > cap;
+    if (over) atomicOr(err, ERR_MVX_CAP);
+    unsigned long long rp = (unsigned long long)q * cap + nb;
+    for (uint32_t i = 0; i < nb; ++i) {
+      hpos[f + i] = (unsigned long long)q * cap + i;  // (cap >= nb: the host sizes every slot so)
+      rpos[f + i] = over ? ~0ull : rp;
+      rp += bincnt[f + i];
+    }
   }
 }
 
@@ -1637,7 +1676,7 @@ hipError_t mvx_expand(Engine& e, uint32_t g, uint32_t d, uint32_t n_local, std::
   if (G) {
     const size_t lds_x = mv_hist_bytes(nbc) + (size_t)e.mv.XT * e.ASZP * 8;
     launch_expand(e, a, d, MV_NOPAIR, lds_x, std::min<uint32_t>(G, 2048));
-    hipLaunchKernelGGL(k_mvx_bincount, dim3(nbc), dim3(256), 0, e.st, a, G, e.x_bincnt);
+    hipLaunchKernelGGL(k_mvx_bincount, dim3(nbc), dim3(256), 0, e.st, a, G, d, e.x_bincnt);
     if ((r = hipMemcpyAsync(cnt.data(), e.x_bincnt, nbc * 4, hipMemcpyDeviceToHost, e.st))) return r;
     if ((r = hipStreamSynchronize(e.st))) return r;
   } else {
@@ -1667,7 +1706,7 @@ hipError_t mvx_expand(Engine& e, uint32_t g, uint32_t d, uint32_t n_local, std::
     }
   }
   if ((r = hipMemcpyAsync(e.x_pos, pos.data(), pos.size() * 8, hipMemcpyHostToDevice, e.st))) return r;
-  hipLaunchKernelGGL(k_mvx_pack, dim3(nbc), dim3(256), 0, e.st, a, G, e.x_pos, e.x_pos + nbc, e.x_bincnt, e.x_send);
+  hipLaunchKernelGGL(k_mvx_pack, dim3(nbc), dim3(256), 0, e.st, a, G, d, e.x_pos, e.x_pos + nbc, e.x_bincnt, e.x_send);
   e.x_send_words = start[K];
   if ((r = hipStreamSynchronize(e.st))) return r;  // (pos is a host temporary)
   return hipGetLastError();
@@ -1684,7 +1723,7 @@ hipError_t mvx_apply(Engine& e, uint32_t g, uint32_t d, const unsigned long long
   uint32_t blo, nbm;
   mvx_bins(e, e.part_rank, blo, nbm);
   if ((r = hipMemcpyAsync(e.x_off, off.data(), (K + 1) * 8, hipMemcpyHostToDevice, e.st))) return r;
-  hipLaunchKernelGGL(k_mvx_trows, dim3(K), dim3(64), 0, e.st, recv, e.x_off, blo, nbm, e.mv.nbc, K, e.x_T);
+  hipLaunchKernelGGL(k_mvx_trows, dim3(K), dim3(64), 0, e.st, recv, e.x_off, 0ull, blo, nbm, e.mv.nbc, K, e.x_T);
   a.T = e.x_T;
   a.TS = K;
   a.area = const_cast<unsigned long long*>(recv);
@@ -1696,6 +1735,50 @@ hipError_t mvx_apply(Engine& e, uint32_t g, uint32_t d, const unsigned long long
   if ((r = hipStreamSynchronize(e.st))) return r;
   n_next = e.h_err[1];
   return hipGetLastError();
+}
+
+// ---------------------------------- frontier exchange, asynchronous level loop ----
+// Level d without a host wait: expand (its grid-stride loop reads the level size on the
+// device), per-bin counts, the fixed-slot layout and the pack into `send` (K slots of `cap`
+// words). The all-to-all that follows moves equal slots, so the host needs no size.
+hipError_t mvx_expand_async(Engine& e, uint32_t g, uint32_t d, unsigned long long cap, unsigned long long* send) {
+  MvArgs a = mv_args(e, e.mv_groups[g], g);
+  const uint32_t nbc = e.mv.nbc, K = e.part_K;
+  const size_t lds_x = mv_hist_bytes(nbc) + (size_t)e.mv.XT * e.ASZP * 8;
+  launch_expand(e, a, d, MV_NOPAIR, lds_x, 2048);
+  hipLaunchKernelGGL(k_mvx_bincount, dim3(nbc), dim3(256), 0, e.st, a, 0xFFFFFFFFu, d, e.x_bincnt);
+  hipLaunchKernelGGL(k_mvx_layout, dim3(1), dim3(64), 0, e.st, K, e.x_bins, e.x_bincnt, cap, e.x_pos, e.x_pos + nbc,
+                     e.x_wlog + (size_t)d * K, e.err);
+  hipLaunchKernelGGL(k_mvx_pack, dim3(nbc), dim3(256), 0, e.st, a, 0xFFFFFFFFu, d, e.x_pos, e.x_pos + nbc, e.x_bincnt,
+                     send);
+  return hipGetLastError();
+}
+
+// Level d's apply of what every rank sent (K slots of `cap` words in `recv`): T rows from the
+// slots' headers, then k_mv_apply; the next level's own entries count stays on the device.
+hipError_t mvx_apply_async(Engine& e, uint32_t g, uint32_t d, const unsigned long long* recv, unsigned long long cap) {
+  MvArgs a = mv_args(e, e.mv_groups[g], g);
+  const uint32_t K = e.part_K;
+  uint32_t blo, nbm;
+  mvx_bins(e, e.part_rank, blo, nbm);
+  hipLaunchKernelGGL(k_mvx_trows, dim3(K), dim3(64), 0, e.st, recv, nullptr, cap, blo, nbm, e.mv.nbc, K, e.x_T);
+  a.T = e.x_T;
+  a.TS = K;
+  a.area = const_cast<unsigned long long*>(recv);
+  a.xrows = K;
+  const size_t lds_a = mv_apply_lds_bytes(e.mv.BSC);
+  const uint32_t agrid = ((e.mv.nbc + 7) / 8) * 8;
+  hipLaunchKernelGGL(k_mv_apply, dim3(agrid), dim3(MV_AT), lds_a, e.st, a, d, MV_NOPAIR, e.mv_q[0], e.mv_q[1]);
+  return hipGetLastError();
+}
+
+// Every rank's first coarse bin and bin count (k_mvx_layout's xbin), once per engine.
+hipError_t mvx_upload_bins(Engine& e) {
+  std::vector<uint32_t> xb(2 * (size_t)e.part_K);
+  for (uint32_t q = 0; q < e.part_K; ++q) mvx_bins(e, q, xb[2 * q], xb[2 * q + 1]);
+  hipError_t r = hipMemcpyAsync(e.x_bins, xb.data(), xb.size() * 4, hipMemcpyHostToDevice, e.st);
+  if (r == hipSuccess) r = hipStreamSynchronize(e.st);  // (xb is a host temporary)
+  return r;
 }
 
 // After the group's last level: gather + consume of its own nodes straight from the LDS CSR

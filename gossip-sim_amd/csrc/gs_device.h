@@ -15,6 +15,10 @@ constexpr uint32_t ERR_INBOUND = 1u, ERR_CACHE = 2u, ERR_DEPTH = 4u, ERR_MV_CAP 
 // which multi-source BFS capacity ERR_MV_CAP hit (reported with it)
 constexpr uint32_t ERR_MVD_ROWS = 0x1000u, ERR_MVD_AREA = 0x2000u, ERR_MVD_POOL = 0x4000u, ERR_MVD_Q = 0x8000u,
                    ERR_MVD_CSR = 0x10000u;
+// a frontier-exchange message outgrew its fixed-capacity slot (the asynchronous level loop:
+// not an error of the engine -- gs_part_xbfs_async_status reports and clears it, and the
+// group's BFS is redone with exact sizes)
+constexpr uint32_t ERR_MVX_CAP = 0x20000u;
 constexpr uint32_t CACHE_CAP = 96;   // >= 50 zero-score + 2 timely keys x 20 rounds (received_cache.rs:78-97)
 constexpr uint32_t CACHE_LIMIT = 50; // ReceivedCacheEntry::CAPACITY
 constexpr uint32_t MIN_NUM_UPSERTS = 20;

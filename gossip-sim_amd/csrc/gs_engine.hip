@@ -178,8 +178,9 @@ static int check_err(Engine* e) {
   const uint32_t f = e->h_err[0];
   if (f & ERR_SYNC) {  // (first: a barrier that timed out leaves every later result suspect)
     e->broken = true;  // its barrier epochs are out of step: every later call is refused
-    return fail(GS_EHIP, "multi-source BFS: a grid barrier of the persistent level kernel timed out (workgroups not "
-                         "co-resident?); the engine is unusable -- destroy it and rerun without GS_MV_PERSIST=1");
+    return fail(GS_EHIP, "multi-source BFS: a grid barrier of a persistent kernel timed out (workgroups not "
+                         "co-resident?); the engine is unusable -- destroy it and rerun with GS_MV_PBFS=0 (and "
+                         "without GS_MV_PERSIST=1)");
   }
   if (f & ERR_INBOUND)
     return fail(GS_ERANGE, "inbound capacity exceeded: a node received more than " + std::to_string(e->capin) +
@@ -512,6 +513,8 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
       ALLOC(e->x_bincnt, e->mv.nbc, 0);
       ALLOC(e->x_pos, 2 * (size_t)e->mv.nbc, 0);
       ALLOC(e->x_off, (size_t)K + 1, 0);
+      ALLOC(e->x_bins, 2 * (size_t)K, 0);
+      ALLOC(e->x_wlog, 256 * (size_t)K, 0);
     }
   }
   if (const char* pp = std::getenv("GS_PHASE_PROFILE"); pp && pp[0] == '1') ALLOC(e->phase_clk, 32, 0);
@@ -1558,6 +1561,72 @@ int gs_part_xbfs_end(gs_engine* eh, int record) {
   e->x_group = 0xFFFFFFFFu;
   e->inb_valid = false;
   return check_err(e);
+}
+
+// The asynchronous level loop (fixed-capacity message slots; RCCL all-to-all on the engine's
+// stream): nothing below waits on the host until gs_part_xbfs_async_status.
+static uint32_t mvx_max_bins(const Engine& e) {
+  uint32_t m = 0;
+  for (uint32_t q = 0; q < e.part_K; ++q) {
+    const size_t lo = std::min<size_t>(e.N, (size_t)q * e.part_C), hi = std::min<size_t>(e.N, lo + e.part_C);
+    const uint32_t f = (uint32_t)(lo >> e.mv.BSC);
+    const uint32_t nb = hi <= lo ? 0u : (uint32_t)(((hi + (1u << e.mv.BSC) - 1) >> e.mv.BSC) - f);
+    m = std::max(m, nb);
+  }
+  return m;
+}
+
+int gs_part_xbfs_expand_async(gs_engine* eh, uint32_t level, uint64_t cap_words, void* send) {
+  PARTX(eh);
+  if (e->x_group == 0xFFFFFFFFu || level != e->x_level || !send)
+    return fail(GS_ESTATE, "gs_part_xbfs_expand_async: begin the group first and take the levels in order");
+  if (level >= 254) return fail(GS_ERANGE, "BFS depth exceeds 254 hops (hop counts are u8)");
+  if (cap_words < mvx_max_bins(*e) || cap_words > 0xFFFFFFF0ull / e->part_K)
+    return fail(GS_EINVAL, "gs_part_xbfs_expand_async: a slot must hold every rank's bin headers (and K slots < 2^32 words)");
+  if (!e->x_bins_set) {
+    HIPC(mvx_upload_bins(*e));
+    e->x_bins_set = true;
+  }
+  HIPC(mvx_expand_async(*e, e->x_group, level, cap_words, reinterpret_cast<unsigned long long*>(send)));
+  return GS_OK;
+}
+
+int gs_part_xbfs_apply_async(gs_engine* eh, uint32_t level, const void* recv, uint64_t cap_words) {
+  PARTX(eh);
+  if (e->x_group == 0xFFFFFFFFu || level != e->x_level || !recv)
+    return fail(GS_ESTATE, "gs_part_xbfs_apply_async: after gs_part_xbfs_expand_async of the same level");
+  HIPC(mvx_apply_async(*e, e->x_group, level, reinterpret_cast<const unsigned long long*>(recv), cap_words));
+  e->x_level = level + 1;
+  return GS_OK;
+}
+
+int gs_part_xbfs_async_status(gs_engine* eh, uint32_t* n_local, uint32_t* overflow, uint64_t* words_log,
+                              size_t log_levels) {
+  PARTX(eh);
+  if (!n_local || !overflow) return fail(GS_EINVAL, "null argument");
+  if (e->x_group == 0xFFFFFFFFu) return fail(GS_ESTATE, "gs_part_xbfs_async_status: no group begun");
+  HIPC(hipMemcpyAsync(e->h_err + 1, e->lvl + e->x_level, 4, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipMemcpyAsync(e->h_err, e->err, 4, hipMemcpyDeviceToHost, e->st));
+  const size_t nl = std::min<size_t>(log_levels, e->x_level);
+  if (words_log && nl)
+    HIPC(hipMemcpyAsync(words_log, e->x_wlog, nl * e->part_K * 8, hipMemcpyDeviceToHost, e->st));
+  HIPC(hipStreamSynchronize(e->st));
+  *overflow = (e->h_err[0] & ERR_MVX_CAP) ? 1u : 0u;
+  if (*overflow) {  // (reported once: the caller redoes the group)
+    e->h_err[0] &= ~ERR_MVX_CAP;
+    HIPC(hipMemcpyAsync(e->err, e->h_err, 4, hipMemcpyHostToDevice, e->st));
+    HIPC(hipStreamSynchronize(e->st));
+  }
+  e->x_nlocal = e->h_err[1];
+  *n_local = e->x_nlocal;
+  return check_err(e);
+}
+
+int gs_stream(gs_engine* eh, void** stream) {
+  ENGINE(eh);
+  if (!stream) return fail(GS_EINVAL, "null argument");
+  *stream = (void*)e->st;
+  return GS_OK;
 }
 
 int gs_part_xround_finish(gs_engine* eh, uint32_t round, int record, uint32_t* n_records) {

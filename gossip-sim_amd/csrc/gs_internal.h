@@ -214,6 +214,9 @@ struct Engine {
   uint32_t* x_bincnt = nullptr;         // [nbc]
   unsigned long long* x_pos = nullptr;  // [2][nbc] header / record places in x_send
   unsigned long long* x_off = nullptr;  // [K + 1]
+  uint32_t* x_bins = nullptr;           // [2K] every rank's first coarse bin and bin count (async loop)
+  bool x_bins_set = false;
+  unsigned long long* x_wlog = nullptr; // [256][K] words of each level's message to each rank (async loop)
   uint32_t x_group = 0xFFFFFFFFu, x_level = 0;
   uint32_t x_nlocal = 0;
   hipEvent_t x_t0 = nullptr;           // (timing of the group's levels)
@@ -326,6 +329,10 @@ hipError_t mvx_expand(Engine& e, uint32_t g, uint32_t d, uint32_t n_local, std::
 hipError_t mvx_apply(Engine& e, uint32_t g, uint32_t d, const unsigned long long* recv,
                      const std::vector<uint64_t>& words_from, uint32_t& n_next);
 hipError_t mvx_gather_consume(Engine& e, uint32_t g, bool record);
+// the asynchronous level loop (fixed-capacity message slots, no host wait per level)
+hipError_t mvx_expand_async(Engine& e, uint32_t g, uint32_t d, unsigned long long cap, unsigned long long* send);
+hipError_t mvx_apply_async(Engine& e, uint32_t g, uint32_t d, const unsigned long long* recv, unsigned long long cap);
+hipError_t mvx_upload_bins(Engine& e);
 // own-bucket entry rows: all nodes (list == nullptr), or the `*count` nodes of `list`
 hipError_t launch_own_rows(Engine& e, const uint32_t* list, const uint32_t* count);
 // the rotation that runs inside the fused round kernel (its workgroup 0) on the other row buffer

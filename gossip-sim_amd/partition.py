@@ -23,6 +23,7 @@ Results on owned nodes, and every summary, are bit-identical to one engine over 
 nodes (tests/test_partition.py).
 """
 import ctypes as C
+import os
 import time
 
 import numpy as np
@@ -59,7 +60,7 @@ def partition_ranges(n, world, frontier=False):
 
 class PartitionedEngine:
     def __init__(self, stakes, n_slots, *, group=None, device=0, exchange="auto", bfs="replicated",
-                 profile=False, serialize=False, **engine_kw):
+                 profile=False, serialize=False, async_levels=True, **engine_kw):
         import torch
         import torch.distributed as tdist
         self.torch, self.tdist, self.group = torch, tdist, group
@@ -107,6 +108,21 @@ class PartitionedEngine:
         # own kernels alone: the per-rank share of a K-GPU run, measured on one device.
         self.prof = {} if profile else None
         self.serialize = serialize
+        # frontier exchange: after a round of the synchronous level loop, the next rounds run
+        # their levels without a host wait (fixed-capacity message slots sized from the last
+        # round, _async_levels); async_levels=False keeps the per-level size exchange
+        # (not with serialize over several ranks: the loop's collectives cannot take turns)
+        self.async_levels = async_levels and self.frontier and not (serialize and self.world > 1)
+        self.pred = {}          # slot group -> message slot words per level (agreed by every rank)
+        self.async_rounds = 0   # groups run by the asynchronous loop / redone after an overflow
+        self.async_redo = 0
+        self._ext = None
+        if self.async_levels and self.on_device:
+            sp = C.c_void_p()
+            _check(lib().gs_stream(self.eng.h, C.byref(sp)))
+            self._ext = torch.cuda.ExternalStream(sp.value, device=self.dev)
+        bsc = coarse_bin_nodes(len(stakes))
+        self._hdr = max(-(-(hi - lo) // bsc) + 2 for lo, hi in ranges)  # bin headers per message, at most
 
     # the Engine's other calls (set_slots, init_active_sets, fail_nodes, readbacks) are
     # replicated or rank-local and need no exchange
@@ -169,6 +185,53 @@ class PartitionedEngine:
         if self.on_device:
             self.torch.cuda.synchronize()
 
+    def _async_levels_run(self, caps):
+        """Levels 0 .. len(caps) - 1 of the begun group without a host wait: every rank packs
+        its message to rank q into slot q of a K x cap buffer (gs_part_xbfs_expand_async),
+        the all-to-all moves equal slots (RCCL: enqueued on the engine's stream, so it
+        orders with the kernels), the apply reads the slots' headers. One status read at the
+        end: (overflow on any rank, next-level entries on any rank, this rank's words log)."""
+        torch, tdist, L, h, K = self.torch, self.tdist, lib(), self.eng.h, self.world
+        cmax = max(caps)
+        dev = torch.device("cuda", torch.cuda.current_device()) if not self.on_device else self.dev
+        send = torch.empty(K * cmax, dtype=torch.int64, device=dev)
+        recv = torch.empty(K * cmax, dtype=torch.int64, device=dev)
+        self.eng.sync()  # (the buffers exist before the engine's stream uses them)
+        for d, cap in enumerate(caps):
+            _check(L.gs_part_xbfs_expand_async(h, d, cap, self._ptr(send)))
+            if self.on_device:
+                with torch.cuda.stream(self._ext):
+                    tdist.all_to_all_single(recv[:K * cap], send[:K * cap], group=self.group)
+            else:  # gloo: the slots through host memory
+                self.eng.sync()
+                hs = send[:K * cap].cpu()
+                hr = torch.empty_like(hs)
+                tdist.all_to_all_single(hr, hs, group=self.group)
+                recv[:K * cap].copy_(hr)
+                torch.cuda.synchronize()
+            _check(L.gs_part_xbfs_apply_async(h, d, self._ptr(recv), cap))
+            self.level_bytes += 8 * K * cap
+        n, ov = C.c_uint32(), C.c_uint32()
+        log = np.zeros((len(caps), K), dtype=np.uint64)
+        _check(L.gs_part_xbfs_async_status(h, C.byref(n), C.byref(ov), log.ctypes.data_as(C.c_void_p), len(caps)))
+        flags = torch.tensor([ov.value, n.value], dtype=torch.int64, device=self.dev)
+        tdist.all_reduce(flags, op=tdist.ReduceOp.MAX, group=self.group)
+        del send, recv
+        return int(flags[0].item()), int(flags[1].item()), n.value, log
+
+    def _predict(self, g, words):
+        """The next round's slot words per level (every rank the same): the largest message of
+        each level over ranks and destinations, +25 % and 1,024 words of headroom."""
+        torch, tdist = self.torch, self.tdist
+        w = torch.zeros(256, dtype=torch.int64, device=self.dev)
+        w[:len(words)] = torch.tensor([int(x) for x in words], dtype=torch.int64)
+        nl = torch.tensor([len(words)], dtype=torch.int64, device=self.dev)
+        tdist.all_reduce(w, op=tdist.ReduceOp.MAX, group=self.group)
+        tdist.all_reduce(nl, op=tdist.ReduceOp.MAX, group=self.group)
+        w = w.cpu().numpy()[:int(nl.item())]
+        force = int(os.environ.get("GS_XBFS_SLOT_WORDS", "0"))  # (tests: slots too small -> overflow -> redo)
+        self.pred[g] = [max(force if force else int(x * 1.25) + 1024, self._hdr) for x in w]
+
     def _frontier_bfs(self, record):
         """Cluster::run_gossip (gossip.rs:494-615) over the partition with a frontier exchange
         per level: each rank expands only its own frontier entries; the level's push records
@@ -186,11 +249,27 @@ class PartitionedEngine:
         T, X = self._timed, self._xchg
         for g in range(ng.value):
             T("begin", lambda: _check(L.gs_part_xbfs_begin(h, g, C.byref(n))))
+            words = []  # this rank's largest message per level (the next round's slot sizes)
+            d = 0
+            caps = self.pred.get(g) if self.async_levels else None
+            if caps:
+                over, more, nloc, log = T("async_levels", lambda: self._async_levels_run(caps))
+                self.async_rounds += 1
+                if over:  # a message outgrew its slot somewhere: redo the group, sizes exchanged per level
+                    self.async_redo += 1
+                    T("begin", lambda: _check(L.gs_part_xbfs_begin(h, g, C.byref(n))))
+                else:
+                    words = [int(x) for x in log.max(axis=1)]
+                    d = len(caps)
+                    n.value = nloc  # (the sync loop below continues when the BFS went deeper)
             tot = torch.tensor([n.value], dtype=torch.int64, device=self.dev)
             X(lambda: tdist.all_reduce(tot, group=self.group))
-            d = 0
             while int(tot.item()) > 0:
                 T("expand", lambda: _check(L.gs_part_xbfs_expand(h, d, wto.ctypes.data_as(C.c_void_p))))
+                if d < len(words):
+                    words[d] = max(words[d], int(wto.max()))
+                else:
+                    words.append(int(wto.max()))
                 cto = torch.tensor(wto.astype(np.int64), device=self.dev)
                 cfrom = torch.zeros(K, dtype=torch.int64, device=self.dev)
                 X(lambda: tdist.all_to_all_single(cfrom, cto, group=self.group))
@@ -208,6 +287,11 @@ class PartitionedEngine:
                 X(lambda: tdist.all_reduce(tot, group=self.group))
                 d += 1
             T("gather_consume", lambda: _check(L.gs_part_xbfs_end(h, int(bool(record)))))
+            if self.async_levels:
+                # (levels past the BFS's end in the async run sent nothing: trimmed)
+                while len(words) > 1 and words[-1] <= self._hdr:
+                    words.pop()
+                self._predict(g, words)
             levels = max(levels, d)
         self.levels = levels
 

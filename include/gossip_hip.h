@@ -266,6 +266,24 @@ int gs_part_xbfs_send(gs_engine* e, void* dst, int dst_device);
 int gs_part_xbfs_apply(gs_engine* e, uint32_t level, const void* src, const uint64_t* words_from /*[K]*/,
                        int src_device, uint32_t* n_local);
 int gs_part_xbfs_end(gs_engine* e, int record);
+/* The same level loop without a host wait per level (round 6): every rank's message to rank q
+ * goes to the fixed slot [q * cap_words, (q + 1) * cap_words) of `send` (device memory, K
+ * slots), so the all-to-all moves K equal slots and no size reaches the host. The caller
+ * runs the predicted number of levels (the previous round's, agreed by all ranks; levels
+ * past the BFS's end are no-ops), enqueues the collective on the engine's stream
+ * (gs_stream), then calls gs_part_xbfs_async_status once: n_local = this rank's entries of
+ * the next level (all ranks 0: the BFS is over, else continue with gs_part_xbfs_expand /
+ * _apply from that level), overflow = 1 if a message outgrew its slot (then every rank
+ * redoes the group: gs_part_xbfs_begin again), words_log [levels][K] = the words each
+ * level sent to each rank (the next round's slot sizes). cap_words must hold every rank's
+ * bin headers. Replaces the per-level size exchange of gossip.rs:511-609's partitioned
+ * form; no reference interface. */
+int gs_part_xbfs_expand_async(gs_engine* e, uint32_t level, uint64_t cap_words, void* send);
+int gs_part_xbfs_apply_async(gs_engine* e, uint32_t level, const void* recv, uint64_t cap_words);
+int gs_part_xbfs_async_status(gs_engine* e, uint32_t* n_local, uint32_t* overflow, uint64_t* words_log,
+                              size_t log_levels);
+/* The engine's HIP stream (hipStream_t), e.g. to enqueue a collective behind its kernels. */
+int gs_stream(gs_engine* e, void** stream);
 int gs_part_xround_finish(gs_engine* e, uint32_t round, int record, uint32_t* n_records);
 int gs_part_stats_out(gs_engine* e, void* dst, int dst_device);          /* [S][5 + 256 + W] u64 */
 int gs_part_stats_in(gs_engine* e, const void* src, int src_device);

@@ -48,6 +48,7 @@ def main():
     out["xrecords"] = np.array([n for _, _, n in modes], dtype=np.uint64)
     out["xbytes"] = np.array([pe.bytes_in], dtype=np.uint64)
     out["levels"] = np.array([pe.levels, pe.level_bytes], dtype=np.uint64)
+    out["async"] = np.array([pe.async_rounds, pe.async_redo], dtype=np.uint64)
     info = pe.info()
     out["bytes"] = np.array([info["device_bytes"], info["pair_bytes"], info["other_bytes"]], dtype=np.uint64)
     np.savez(os.environ["GS_PART_OUT"], **out)

@@ -38,6 +38,7 @@ def main():
         for k, v in res.items():
             out[f"part_{exchange}_{k}"] = v
         out[f"part_{exchange}_modes"] = np.array(modes)
+        out[f"part_{exchange}_async"] = np.array([pe.async_rounds, pe.async_redo])
         pe.close()
     _, st90 = eb.synth.network(90)
     res = sw.run_sharded(st90, n_sims=3, origin_ranks=[1, 2, 1], fractions=[0.1, 0.0, 0.3], device=0,

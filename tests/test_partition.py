@@ -85,15 +85,28 @@ def test_partition_ranges_frontier_units():
     ("small", "gloo", "auto", "replicated"), ("small", "gloo", "dense", "replicated"),
     ("small", "nccl", "auto", "replicated"), ("large", "gloo", "auto", "replicated"),
     ("large", "gloo", "records", "replicated"),
-    ("small", "gloo", "auto", "frontier"), ("large", "gloo", "auto", "frontier")])
+    ("small", "gloo", "auto", "frontier"), ("large", "gloo", "auto", "frontier"),
+    ("small", "gloo", "auto", "frontier-redo")])
 def test_partition_two_ranks_matches_one_engine(tmp_path, case, backend, exchange, bfs):
     """(exchange: the prune exchange -- auto = records outside prune waves, dense in them;
     records / dense forced. bfs: replicated = every rank runs the whole BFS; frontier = each
-    rank expands its own frontier and the level's push records go to their owners.)"""
-    extra = {"GS_PART_RECORD_CAP": str(1 << 25)} if exchange == "records" else None
+    rank expands its own frontier and the level's push records go to their owners -- the
+    first round with a size exchange per level, the later ones without a host wait per level
+    (fixed message slots from the last round's sizes); frontier-redo: slots forced too small,
+    so a round's message overflows its slot and the group is redone with exact sizes.)"""
+    extra = {"GS_PART_RECORD_CAP": str(1 << 25)} if exchange == "records" else {}
+    if bfs == "frontier-redo":
+        extra["GS_XBFS_SLOT_WORDS"] = "40"
+        bfs = "frontier"
+        redo = True
+    else:
+        redo = False
     parts, caches = run_ranks(tmp_path, case, backend, exchange=exchange, extra_env=extra, bfs=bfs)
     if bfs == "frontier":
         assert all(int(p["levels"][0]) >= 3 and int(p["levels"][1]) > 0 for p in parts), [p["levels"] for p in parts]
+        asy = [tuple(int(x) for x in p["async"]) for p in parts]
+        assert all(a > 0 for a, _ in asy), asy  # rounds after the first ran the asynchronous level loop
+        assert all((r > 0) == redo for _, r in asy), asy
     modes = set(str(m) for m in parts[0]["xmodes"] if str(m))
     if exchange != "auto":
         assert modes == {exchange}, modes

@@ -49,6 +49,9 @@ def test_rccl_world1_exchanges_match_gloo_and_one_engine(tmp_path):
     for k in nccl:
         if k != "backend":
             assert nccl[k].tobytes() == gloo[k].tobytes(), k
+    # the frontier exchange ran its levels without host waits after the first round (slots from
+    # the last round's sizes), the collective enqueued on the engine's stream
+    assert int(nccl["part_frontier_async"][0]) > 0, nccl["part_frontier_async"]
     for ex in ("records", "dense"):  # each exchange form really ran, in the prune wave too
         modes = set(str(m) for m in nccl[f"part_{ex}_modes"] if str(m))
         assert modes == {ex}, (ex, modes)
