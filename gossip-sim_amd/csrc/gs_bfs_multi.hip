@@ -450,198 +450,6 @@ __global__ __launch_bounds__(MV_ST) void k_mv_small(MvArgs a, uint32_t mode, uin
       __hip_atomic_store(&a.hlvl[k], a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// ----------------------------------------------------- persistent levels ----
-// The small levels as ONE launch over the whole chip: G resident workgroups (one per CU),
-// a grid barrier between levels. A level's entries are dealt over every CU, so its
-// device-scope atomics (vis ORs, pool places, next-level reservations) and scattered row
-// loads are spread over 256 address units instead of one CU's (k_mv_small's levels are
-// bound by one CU's rate of scattered accesses: ~20 us for a level of 217 entries at C4).
-// Per level the same steps as k_mv_small (mv_expand_entry, the vis atomic that sets a
-// slot's bit is that slot's first arrival at hop d + 1, gossip.rs:594-600; records to
-// their fine bins' pools stamped with the hop); next-level entries are reserved once per
-// wave on lvl[d + 1] and written to the global queue. Modes as k_mv_small's.
-constexpr uint32_t MV_PT = 512;       // threads per workgroup of the persistent kernel
-// barrier block (e.mv_bar, 256 words): shard counters at 16 s (s < 8), top 128, generation 144, base 160
-constexpr uint32_t MV_PSMALL = 16384;   // default head / tail level bound of the persistent kernel
-
-// Grid barrier of a persistent launch (Guideline 16's counter form, sharded by blockIdx & 7).
-// Everything one workgroup hands to another inside the launch is written through to memory
-// and read around L1: the next level's queue entries by agent-scope (sc1) stores and loads,
-// the level sizes, visited masks and pool fills by device-scope atomics. So the barrier
-// needs no L2 write-back (release fence) and no L1 invalidate (acquire fence): every wave
-// drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier, thread 0 arrives on
-// its shard; the last of a shard arrives on the top counter, the last shard publishes the
-// generation e (an atomic store); thread 0 polls it relaxed.
-// Counters are cumulative: epoch e's arrivals end at e x (workgroups of the shard), so no
-// word is reset between barriers or launches (the grid size G of an engine never changes;
-// the last epoch used is kept in word 160 for the next launch). A spin is bounded (~1 s):
-// on expiry ERR_SYNC is raised and the workgroup goes on (wrong results, no hang).
-__device__ inline void mv_grid_sync(uint32_t* bar, uint32_t e, uint32_t G, uint32_t* err) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t sh = blockIdx.x & 7u, ns = min(G, 8u), cs = (G - sh + 7u) / 8u;
-    const uint32_t r = __hip_atomic_fetch_add(&bar[16 * sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (r + 1u == e * cs) {
-      const uint32_t t = __hip_atomic_fetch_add(&bar[128], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t + 1u == e * ns) __hip_atomic_store(&bar[144], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    for (uint32_t it = 0; __hip_atomic_load(&bar[144], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != e; ++it) {
-      if (it > (1u << 22)) {
-        atomicOr(err, ERR_SYNC);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-}
-
-// Agent-scope (sc1: through L2 to memory, around L1) 8-byte queue entry store / load.
-__device__ inline void mv_q_store(uint2* p, uint2 x) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)x.x | ((unsigned long long)x.y << 32),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline uint2 mv_q_load(const uint2* p) {
-  const unsigned long long v =
-      __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-}
-__device__ inline void mv_st_agent(uint32_t* p, uint32_t x) {
-  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int ASZP>
-__global__ __launch_bounds__(MV_PT, 4) void k_mv_levels(MvArgs a, uint32_t mode, uint32_t d0, uint32_t pi,
-                                                     uint2* __restrict__ q0, uint2* __restrict__ q1,
-                                                     uint32_t* __restrict__ hstate, const uint2* __restrict__ seeds,
-                                                     uint32_t nseed, uint32_t seq, uint32_t* __restrict__ bar) {
-  __shared__ MvSlots S;
-  __shared__ uint32_t gt[GT_WORDS], s_base, s_qn;
-  const uint32_t tid = threadIdx.x, G = gridDim.x, lane = tid & 63;
-  const uint32_t gtid = blockIdx.x * MV_PT + tid, GT = G * MV_PT;
-  mv_slots_load(a, S, tid, MV_PT);
-  for (uint32_t i = tid; i < GT_WORDS; i += MV_PT) gt[i] = a.gt[i];
-  if (tid == 0) s_base = __hip_atomic_load(&bar[160], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // GS_PHASE_PROFILE: clocks of workgroup 0's thread 0 at pclk[5..8] (setup, the first
-  // chunk's loads, atomics + stores, barriers; [9] levels)
-  const bool clk = a.pclk && blockIdx.x == 0 && tid == 0;
-  unsigned long long tm = clk ? wall_clock64() : 0;
-  auto mark = [&](int ph) {
-    if (clk) {
-      const unsigned long long now = wall_clock64();
-      atomicAdd(&a.pclk[ph], now - tm);
-      tm = now;
-    }
-  };
-  uint32_t d = mode == MV_TAIL ? a.dpair[pi] : d0;
-  if (mode == MV_HEAD) {  // the group's round starts here: lvl, pool fills, the seeds' vis and queue
-    for (uint32_t i = gtid; i < 256; i += GT) mv_st_agent(&a.lvl[i], i == 0 ? nseed : 0u);
-    for (uint32_t f = gtid; f < a.fno; f += GT) mv_st_agent(&a.pused[f], 0u);
-    if (gtid == 0) a.ctr[0] = 0;
-    if (gtid < nseed) {
-      const uint2 sd = seeds[gtid];  // distinct origins (vis was cleared before this kernel)
-      mv_q_store(&q0[gtid], sd);
-      mv_st_agent(&a.vis[sd.x & 0xFFFFFFu], sd.y);
-    }
-  }
-  __syncthreads();
-  uint32_t ep = s_base;
-  if (mode == MV_HEAD) mv_grid_sync(bar, ++ep, G, a.err);
-  if (tid == 0) s_qn = d < 256 ? __hip_atomic_load(&a.lvl[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-  __syncthreads();
-  uint32_t qn = min(s_qn, (uint32_t)a.q_cap);
-  const uint32_t lim = mode == MV_TAIL ? 0xFFFFFFFFu : a.small;
-  mark(5);
-  while (qn > 0 && qn <= lim && d < 254) {
-    if (clk) atomicAdd(&a.pclk[9], 1ull);
-    const uint2* __restrict__ qc = (d & 1) ? q1 : q0;
-    uint2* __restrict__ qx = (d & 1) ? q0 : q1;
-    // 64-entry chunks dealt over the workgroups first (chunk c -> workgroup c mod G, wave
-    // c / G): a level of a few thousand entries runs on as many CUs as it has chunks
-    const uint32_t wbase = (((tid >> 6) * G + blockIdx.x) << 6);
-    for (uint32_t i0 = wbase; i0 < qn; i0 += GT) {  // (uniform per wave: wave scans below)
-      const uint32_t i = i0 + lane;
-      uint32_t row[ASZP], acc[ASZP], u = 0;
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) { row[s] = 0; acc[s] = 0; }
-      if (i < qn) mv_expand_entry<ASZP>(a, mv_q_load(&qc[i]), S, row, acc, u);
-      if (clk && i0 == wbase) {  // (profiling only: wait for the entry's loads)
-        uint32_t x = 0;
-#pragma unroll
-        for (int s = 0; s < ASZP; ++s) x |= acc[s];
-        if (x == 0xFFFFFFFFu) atomicOr(a.err, 0u);
-        mark(6);
-      }
-      // every global access of the entry before any result is used: the vis atomics, the
-      // peers' buckets, the pool places
-      uint32_t old[ASZP], pp[ASZP], bw[ASZP];
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) old[s] = acc[s] ? atomicOr(&a.vis[row[s]], acc[s]) : 0xFFFFFFFFu;
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) bw[s] = acc[s] ? (uint32_t)a.bucket[row[s]] : 0u;
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) {
-        const uint32_t f = (row[s] >> a.BSF) - a.flo;
-        pp[s] = acc[s] && f < a.fno ? atomicAdd(&a.pused[f], 1u) : 0xFFFFFFFFu;  // kept bins only
-      }
-      uint32_t n = 0;
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) {
-        const uint32_t nw = acc[s] & ~old[s];
-        if (nw) n += mv_parts(gt, row[s], nw, bw[s], nullptr, 0);
-      }
-      const uint32_t incl = wave_incl_scan(n);
-      const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
-      uint32_t wb = 0;
-      if (lane == 63 && tot) wb = atomicAdd(&a.lvl[d + 1], tot);
-      uint32_t pos = (uint32_t)__shfl((int)wb, 63) + incl - n;
-      const bool qok = (size_t)pos + n <= a.q_cap;
-      if (!qok) atomicOr(a.err, ERR_MV_CAP | ERR_MVD_Q);
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) {
-        if (!acc[s]) continue;
-        const uint32_t w = row[s];
-        if (pp[s] != 0xFFFFFFFFu) {
-          const uint32_t f = (w >> a.BSF) - a.flo;
-          if (pp[s] < a.pcap) a.pool[(size_t)f * a.pcap + pp[s]] = mv_pool_rec(a, u, w & ((1u << a.BSF) - 1), d + 1, acc[s]);
-          else atomicOr(a.err, ERR_MV_CAP | ERR_MVD_POOL);
-        }
-        const uint32_t nw = acc[s] & ~old[s];
-        if (nw && qok) pos += mv_parts_to(gt, w, nw, bw[s], [&](uint32_t k, uint2 x) { mv_q_store(&qx[pos + k], x); });
-      }
-    }
-    mark(7);
-    mv_grid_sync(bar, ++ep, G, a.err);
-    mark(8);
-    ++d;
-    if (tid == 0) s_qn = __hip_atomic_load(&a.lvl[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    qn = min(s_qn, (uint32_t)a.q_cap);
-  }
-  if (blockIdx.x != 0 || tid != 0) return;
-  if (mode == MV_TAIL && qn > 0) atomicOr(a.err, ERR_DEPTH);  // level 254 not empty
-  if (mode == MV_HEAD) a.dpair[0] = d;
-  if (mode == MV_TAIL) {  // the round's level profile for the host's next prediction (seqlock)
-    uint32_t* hp = a.hprof;
-    const uint32_t nl = min(d, 255u);
-    __hip_atomic_store(&hp[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __atomic_thread_fence(__ATOMIC_RELEASE);
-    for (uint32_t k = 0; k < nl; ++k)
-      __hip_atomic_store(&hp[2 + k], __hip_atomic_load(&a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&hp[1], nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&hp[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if (mode != MV_TAIL)  // per-level sizes for the polled loop / diagnostics
-    for (uint32_t k = d0; k < d && k < 256; ++k)
-      __hip_atomic_store(&a.hlvl[k], __hip_atomic_load(&a.lvl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (ep != s_base) __hip_atomic_store(&bar[160], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&hstate[1], qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&hstate[0], d, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // the host polls this word
-}
-
 // --------------------------------------------------------------- gather ----
 constexpr uint32_t MV_GC = 12;        // records per gather thread kept in registers between the passes
 constexpr uint32_t MV_GLDS_DEF = 78 * 1024;  // gather LDS: two workgroups per CU (GS_MV_GLDS_KB: tuning)
@@ -1340,7 +1148,7 @@ MvArgs mv_args(Engine& e, const MvGroup& gr, uint32_t g) {
   a.vlo = e.vlo; a.vhi = e.vlo + e.NP; a.NP = e.NP; a.MSU = (uint32_t)e.msu;
   a.XT = e.mv.XT;
   a.xrows = 0;
-  a.small = e.mv_pgrid ? MV_PSMALL : MV_SMALL;  // the persistent kernel's bound, or the one-workgroup kernel's
+  a.small = MV_SMALL;  // the one-workgroup kernel's level bound
   if (const char* sm = std::getenv("GS_MV_SMALL")) a.small = (uint32_t)std::strtoul(sm, nullptr, 10);
   if (e.prm.flags & GS_FLAG_NO_SMALL_LEVELS) a.small = 0;  // every level through expand + apply
   a.flo = e.vlo >> e.mv.BSF; a.fno = mv_kept_bins(e);
@@ -1410,18 +1218,11 @@ static void launch_expand(Engine& e, const MvArgs& a, uint32_t d, uint32_t pi, s
   }
 }
 
-// The small-level kernel: the persistent one over the chip (e.mv_pgrid workgroups), or
-// with GS_MV_PERSIST=0 the one-workgroup k_mv_small.
+// The small-level kernel (one workgroup, k_mv_small).
 static void launch_small_levels(Engine& e, const MvArgs& a, uint32_t mode, uint32_t d0, uint32_t pi,
                                 const uint2* seeds, uint32_t nseed, uint32_t seq, size_t lds_s) {
-  if (e.mv_pgrid) {
-    GS_ASZP_DISPATCH_V(e.ASZP, hipLaunchKernelGGL((k_mv_levels<A>), dim3(e.mv_pgrid), dim3(MV_PT), 0, e.st, a, mode,
-                                                  d0, pi, e.mv_q[0], e.mv_q[1], e.mv_hstate_dev, seeds, nseed, seq,
-                                                  e.mv_bar));
-  } else {
-    GS_ASZP_DISPATCH_V(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, mode, d0,
-                                                  pi, e.mv_q[0], e.mv_q[1], e.mv_hstate_dev, seeds, nseed, seq));
-  }
+  GS_ASZP_DISPATCH_V(e.ASZP, hipLaunchKernelGGL((k_mv_small<A>), dim3(1), dim3(MV_ST), lds_s, e.st, a, mode, d0, pi,
+                                                e.mv_q[0], e.mv_q[1], e.mv_hstate_dev, seeds, nseed, seq));
 }
 
 // The level loop of one slot group. Two forms:
@@ -1504,24 +1305,6 @@ static hipError_t mv_attrs(Engine& e) {
       r = hipFuncSetAttribute((const void*)k_mv_small<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s);
     });
     if (r != hipSuccess) return r;
-    // GS_MV_PERSIST=1: the persistent level kernel (one workgroup per CU, all resident: its
-    // grid barriers need every workgroup running) instead of the one-workgroup kernel. Off
-    // by default: at C4 it saves ~2 % of the BFS (715.6 vs 732 us with levels up to 16,384
-    // entries), while a node reached by several workgroups at one level becomes several
-    // frontier entries (the apply kernel merges them per node), so it expands more entries
-    // and fills the record pools less predictably.
-    e.mv_pgrid = 0;
-    const char* px = std::getenv("GS_MV_PERSIST");
-    // (never on a partition rank: its grid barriers assume every workgroup co-resident, which
-    // RCCL kernels sharing the device can break)
-    if (px && px[0] == '1' && !e.part_on) {
-      int dev = 0, cus = 0, per = 0;
-      if ((r = hipGetDevice(&dev)) || (r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)))
-        return r;
-      GS_ASZP_DISPATCH(e.ASZP, { r = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mv_levels<A>, MV_PT, 0); });
-      if (r != hipSuccess) return r;
-      if (per >= 1 && cus >= 8) e.mv_pgrid = (uint32_t)cus;
-    }
     e.mv_attr_set = true;
   }
   return r;
@@ -1591,7 +1374,7 @@ hipError_t launch_bfs_multi(Engine& e, bool record, bool consume) {
     } else {
       // the head kernel stops at the first level above a.small; pairs then take the levels
       // the profile had above the tail threshold
-      const uint32_t tail_thr = tail_env != 0xFFFFFFFFu ? tail_env : e.mv_pgrid ? a.small : 2048u;
+      const uint32_t tail_thr = tail_env != 0xFFFFFFFFu ? tail_env : 2048u;
       uint32_t k0 = 0;
       while (k0 < pv.size() && pv[k0] <= a.small) ++k0;
       uint32_t k1 = (uint32_t)pv.size();  // one past the last level above the tail threshold

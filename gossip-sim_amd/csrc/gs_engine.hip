@@ -178,9 +178,8 @@ static int check_err(Engine* e) {
   const uint32_t f = e->h_err[0];
   if (f & ERR_SYNC) {  // (first: a barrier that timed out leaves every later result suspect)
     e->broken = true;  // its barrier epochs are out of step: every later call is refused
-    return fail(GS_EHIP, "multi-source BFS: a grid barrier of a persistent kernel timed out (workgroups not "
-                         "co-resident?); the engine is unusable -- destroy it and rerun with GS_MV_PBFS=0 (and "
-                         "without GS_MV_PERSIST=1)");
+    return fail(GS_EHIP, "multi-source BFS: a grid barrier of the persistent BFS timed out (workgroups not "
+                         "co-resident?); the engine is unusable -- destroy it and rerun with GS_MV_PBFS=0");
   }
   if (f & ERR_INBOUND)
     return fail(GS_ERANGE, "inbound capacity exceeded: a node received more than " + std::to_string(e->capin) +
@@ -463,7 +462,6 @@ static int create_engine(const gs_params* prm, const uint64_t* stakes, uint32_t 
       b0 = e->dev_bytes;
       ALLOC(e->mv_pool, (size_t)fno * g.pcap, 0);
       ALLOC(e->mv_pused, fno, 0);
-      ALLOC(e->mv_bar, 256, 0);  // the persistent level kernel's barrier words (MV_BAR_WORDS)
       e->pair_bytes += e->dev_bytes - b0;
       if (pb_setup(*e)) {  // the persistent BFS (gs_bfs_pers.hip): its level records, T rows and entries
         ALLOC(e->pb_T[0], (size_t)(e->pb_G + 2) * e->pb_rows_cap, 0);

@@ -137,8 +137,6 @@ struct Engine {
   uint2* mv_seed = nullptr;       // [S] seed entries (distinct origins) of every group
   std::vector<MvGroup> mv_groups;
   bool mv_attr_set = false;
-  uint32_t mv_pgrid = 0;          // workgroups of the persistent level kernel (one per CU); 0: one-workgroup kernel
-  uint32_t* mv_bar = nullptr;     // [256] its grid-barrier words (cumulative epochs, zeroed at create)
   uint32_t bfs_level = 0;  // the level loop's current level (reported when a level wait times out)
   bool mv_diag = false;  // GS_MV_DIAG=1
   bool mv_line = false;   // multi: prune masks live in the row table's node lines (msu = 32)
@@ -237,7 +235,7 @@ struct Engine {
 
   std::vector<gs_slot> slots;
   bool slots_set = false, failed_ranked = false;
-  bool broken = false;  // a persistent-kernel grid barrier timed out (ERR_SYNC): the engine refuses every call
+  bool broken = false;  // a grid barrier of the persistent BFS timed out (ERR_SYNC): the engine refuses every call
 
   // profiling
   struct Timed { std::vector<std::pair<hipEvent_t, hipEvent_t>> ev; double ms = 0; uint64_t n = 0; };

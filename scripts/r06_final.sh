@@ -53,7 +53,7 @@ legpmc() {  # legpmc <leg> <family> <marker> <rounds|all> <timeout>
   fi
 }
 if has pmc_legs; then
-  MV=k_mv_expand,k_mv_apply,k_mv_small,k_mv_levels,k_mv_pbfs,k_mv_gather
+  MV=k_mv_expand,k_mv_apply,k_mv_small,k_mv_pbfs,k_mv_gather
   legpmc c4 $MV k_mv_gather 5,24 400 multi || exit 1
   legpmc c5 $MV k_mv_gather 3,12 600 multi || exit 1
   # (c3: two one-slot engines run concurrently, two gather markers per round: marker
@@ -95,7 +95,7 @@ if has trace; then
   echo "== trace legs"
   timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $OUT/proflegs -o run -- \
     python3 bench.py --only-large --legs c4,c5 > $OUT/proflegs.log 2>&1 || { tail -20 $OUT/proflegs.log; exit 1; }
-  MVT=k_mv_expand,k_mv_apply,k_mv_small,k_mv_levels,k_mv_pbfs,k_mv_gather
+  MVT=k_mv_expand,k_mv_apply,k_mv_small,k_mv_pbfs,k_mv_gather
   python3 scripts/trace_window.py --csv $OUT/proflegs/run_kernel_trace.csv --family $MVT --marker k_mv_gather \
     --rounds 5,24 --bench-args "--only-large --legs c4" --out $P/trace_bfs_multi_c4.json || exit 1
   # (c5's rounds follow c4's 25 in the same trace: c4 rounds 0-24 end at marker 24)

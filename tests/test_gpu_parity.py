@@ -881,44 +881,3 @@ def test_multi_bfs_groups_and_entries():
         for k in (0, 40, 69):
             for x, y in zip(a.inbound(k), b.inbound(k)):
                 np.testing.assert_array_equal(x, y)
-
-
-def test_persistent_level_kernel_matches_default():
-    """GS_MV_PERSIST=1 (the opt-in chip-wide level kernel, grid barriers between levels):
-    C4-shaped 13 slots (failures, per-slot thresholds) on 300k nodes, levels up to 16,384
-    entries in the persistent kernel, 8 rounds through polled and predicted level loops:
-    equal to the default multi engine in summaries, hops, in-degrees, inbound lists,
-    counters and caches. (Its frontier may hold a node several times per level, so its
-    record pools fill differently; every result must not.)"""
-    n, S = 300_000, 13
-    st = eb.synth.power_law_stakes(n)
-    origin = int(np.argmax(st))
-    fr = [0.1, 0.2, 0.3, 0.4, 0.5] + [0.0] * 8
-    thr = [0.15] * 5 + [round(0.05 * (j + 1), 2) for j in range(8)]
-    engs = []
-    for persist in ("0", "1"):
-        os.environ["GS_MV_PERSIST"] = persist  # (its default level bound is 16,384 entries)
-        try:
-            e = gs.Engine(st, S, seed=21, rotation_probability=0.02, bfs_mode=gs.GS_BFS_MULTI)
-            e.set_slots([origin] * S, 2, thr)
-            e.init_active_sets()
-            e.fail_nodes(fr)
-            e.round(0, record=False)  # (the engine reads the variables at its first BFS)
-        finally:
-            os.environ.pop("GS_MV_PERSIST", None)
-        engs.append(e)
-    for r in range(1, 8):
-        for e in engs:
-            e.round(r, record=True)
-    a, b = engs
-    np.testing.assert_array_equal(a.summaries(), b.summaries())
-    for k in (0, 4, 5, 12):
-        np.testing.assert_array_equal(a.hops(k), b.hops(k))
-        for x, y in zip(a.inbound(k, cap=8 * n), b.inbound(k, cap=8 * n)):
-            np.testing.assert_array_equal(x, y)
-        for x, y in zip(a.counters(k), b.counters(k)):
-            np.testing.assert_array_equal(x, y)
-        for x, y in zip(a.caches(k), b.caches(k)):
-            np.testing.assert_array_equal(x, y)
-    for e in engs:
-        e.close()
