@@ -763,6 +763,13 @@ def main():
                    "rounds": [args.warmup, args.warmup + args.steps],
                    "pushes_per_origin_round": E_all / (S * world * args.steps) if not args.shard_origins
                    else E_all / (S_all * args.steps),
+                   # which part of the simulation the window times: before the first prune wave
+                   # (round ~19) every node pushes to its whole fanout (~6N pushes per
+                   # origin-round); after the waves settle (rounds >= 60, `steady_state`) ~3N
+                   "regime": ("pre-prune, through the first prune wave (~6N pushes per origin-round)"
+                              if args.warmup + args.steps <= 40 else
+                              "steady state after the prune waves (~3N pushes per origin-round)"
+                              if args.warmup >= 60 else "mixed: the first prune waves and after"),
                    "parallelism": (f"origin-sharded x{world} (one trial)" if args.shard_origins else
                                    f"trial-sharded x{world} (rank r: all origins, Philox seed + r)")},
         "origin_rounds_per_s": (S_all if args.shard_origins else S * world) * args.steps / dt,
