@@ -184,7 +184,7 @@ constexpr int mv_orw() { return ((ASZP + 1 + ASZP / 4) + 3) & ~3; }
 // slots with prune bits at u run the per-slot selection, which a wave executes for the
 // union of its lanes' slots. Plain slots' push counts come from bit-sliced counters.
 template <int ASZP, bool EG = true>  // EG: write the egress bytes of the entry's slots
-__device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const MvSlots& S, uint32_t (&row)[ASZP],
+__device__ __forceinline__ void mv_expand_entry(const MvArgs& a, uint2 ent, const MvSlots& S, uint32_t (&row)[ASZP],
                                        uint32_t (&acc)[ASZP], uint32_t& u) {
   constexpr int TQ = (mv_orw<ASZP>() - ASZP) / 4;
   u = ent.x & 0xFFFFFFu;
@@ -234,31 +234,31 @@ __device__ inline void mv_expand_entry(const MvArgs& a, uint2 ent, const MvSlots
       const uint32_t pre = (1u << nf) - 1u, nxp = L > a.fanout ? 1u << a.fanout : 0u;  // ring positions
       const uint32_t tkn = ((pre << head) | (pre >> (SZ - head))) & full;               // physical slots
       const uint32_t nxt = ((nxp << head) | (nxp >> (SZ - head))) & full;
-      uint32_t rem = 0;  // plain slots whose origin is in the prefix
-      uint32_t ap[ASZP];
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) {
-        ap[s] = 0;
-        if (!((tkn >> s) & 1u)) continue;
-        const uint32_t om = mv_origin_slots(S, row[s]) & plain;
-        ap[s] = plain & ~om;
-        rem |= om;
-      }
-      if (rem) {
-#pragma unroll
-        for (int s = 0; s < ASZP; ++s)
-          if ((nxt >> s) & 1u) ap[s] |= rem;
-      }
-#pragma unroll
-      for (int s = 0; s < ASZP; ++s) {
-        if (a.any_fail && ap[s]) ap[s] &= ~S.fm[fc[s]];  // failed peers burn their slot (gossip.rs:538-541)
-        acc[s] |= ap[s];
-        uint32_t x = ap[s], t;  // bit-sliced add: pushes per plain slot (<= fanout < 32)
+      // ring slot s pushes to the slots x: failed peers burn their slot (gossip.rs:538-541),
+      // and a bit-sliced add counts the pushes per plain slot (<= fanout < 32). (Applied in
+      // place per s: a per-slot array here went to scratch at ASZP 20, 3x the expand time.)
+      auto take = [&](int s, uint32_t x) {
+        if (a.any_fail) x &= ~S.fm[fc[s]];
+        acc[s] |= x;
+        uint32_t t;
         t = pc0 & x; pc0 ^= x; x = t;
         t = pc1 & x; pc1 ^= x; x = t;
         t = pc2 & x; pc2 ^= x; x = t;
         t = pc3 & x; pc3 ^= x; x = t;
         pc4 ^= x;
+      };
+      uint32_t rem = 0;  // plain slots whose origin is in the prefix
+#pragma unroll
+      for (int s = 0; s < ASZP; ++s) {
+        if (!((tkn >> s) & 1u)) continue;
+        const uint32_t om = mv_origin_slots(S, row[s]) & plain;
+        take(s, plain & ~om);
+        rem |= om;
+      }
+      if (rem) {  // those slots take position `fanout` instead (disjoint from the prefix)
+#pragma unroll
+        for (int s = 0; s < ASZP; ++s)
+          if ((nxt >> s) & 1u) take(s, rem);
       }
     }
   }
