@@ -11,8 +11,8 @@ run() {  # run <name> <args...>
   timeout -k 10 ${TO:-400} python3 bench.py "$@" > $OUT/$n.log 2>&1 || { tail -20 $OUT/$n.log; exit 1; }
   tail -1 $OUT/$n.log | cut -c1-300
 }
-for s in 375 750 1500 3000; do run c2_$s --slots $s --no-cpu-baseline --no-large --no-steady; done
+for s in 375 750 1500 3000; do run c2_$s --warmup 5 --steps 20 --slots $s --no-cpu-baseline --no-large --no-steady; done
 run c4_0,8 --only-large --legs c4 --c4-sims 0,8
 run c4_5 --only-large --legs c4 --c4-sims 5
 run c5_2 --only-large --legs c5 --c5-slots 2
-run c3_w16 --workload c3 --no-cpu-baseline
+run c3_w16 --warmup 5 --steps 20 --workload c3 --no-cpu-baseline
