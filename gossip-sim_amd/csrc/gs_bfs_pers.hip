@@ -30,10 +30,17 @@
 //            region).
 // The BFS ends at the first level with no slices anywhere (a grid-uniform count). Results
 // equal the launched loop's bit for bit: the same entries, records, pools and egress.
+#include <fcntl.h>
+#include <sys/file.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
+#include <string>
 
 #include "gs_device.h"
 #include "gs_internal.h"
@@ -489,7 +496,34 @@ static size_t pb_lds_bytes(uint32_t stage_cap, uint32_t NO, uint32_t G, uint32_t
 // Process-wide count of engines that may launch the persistent BFS: two persistent
 // launches on one device (two engines on two streams) could each hold part of the CUs the
 // other needs resident, so the persistent path runs only while one such engine exists.
+// Across processes the same holds per device: two ranks sharing one GPU (the world-2 tests,
+// a rehearsal of a multi-rank launch on one card) would each see one engine of their own.
+// So the first registered engine of a process also takes an exclusive, non-blocking lock
+// on a file named after the device's PCI bus id; a process that does not get it (another
+// process on the card holds it) uses the launched level loop until its engines are gone.
+// (Kernels of other processes still share the CUs, but they finish: the persistent
+// launch's workgroups that wait at a barrier for the rest only wait longer.)
 static std::atomic<int> g_pb_engines{0};
+static std::mutex g_pb_mu;
+static int g_pb_lock_fd = -1;
+static std::atomic<bool> g_pb_locked{false};
+
+static bool pb_lock_device() {
+  int dev = 0;
+  char bus[64] = {0};
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, dev) != hipSuccess) return false;
+  std::string path = "/tmp/gossip_hip_pbfs_";
+  for (const char* c = bus; *c; ++c) path += std::isalnum((unsigned char)*c) ? *c : '_';
+  path += ".lock";
+  const int fd = open(path.c_str(), O_RDONLY | O_CREAT | O_CLOEXEC, 0666);
+  if (fd < 0) return false;
+  if (flock(fd, LOCK_EX | LOCK_NB) != 0) {
+    close(fd);
+    return false;
+  }
+  g_pb_lock_fd = fd;
+  return true;
+}
 
 bool pb_setup(Engine& e) {
   e.pb_on = false;
@@ -525,12 +559,18 @@ bool pb_setup(Engine& e) {
 }
 
 void pb_register(Engine& e, bool on) {
-  if (on) g_pb_engines.fetch_add(1);
-  else g_pb_engines.fetch_sub(1);
+  std::lock_guard<std::mutex> lk(g_pb_mu);
+  if (on) {
+    if (g_pb_engines.fetch_add(1) == 0) g_pb_locked = pb_lock_device();  // (the engine's device is current)
+  } else if (g_pb_engines.fetch_sub(1) == 1 && g_pb_lock_fd >= 0) {
+    close(g_pb_lock_fd);  // (releases the lock)
+    g_pb_lock_fd = -1;
+    g_pb_locked = false;
+  }
   (void)e;
 }
 
-bool pb_usable(const Engine& e) { return e.pb_on && g_pb_engines.load() == 1; }
+bool pb_usable(const Engine& e) { return e.pb_on && g_pb_engines.load() == 1 && g_pb_locked.load(); }
 
 hipError_t launch_bfs_pers(Engine& e, const MvArgs& a, const MvGroup& gr) {
   hipError_t r = hipSuccess;

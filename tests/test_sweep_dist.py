@@ -154,6 +154,46 @@ def test_sharded_sweep_gpu_world2_matches_one_process():
         _check(got, want)
 
 
+def _pbfs_worker(rank, world, port, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.dirname(here)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as tdist
+    import engine_bind
+    g = engine_bind.gs
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    _, st = engine_bind.synth.network(20_000)
+    eng = g.Engine(st, 2, rotation_probability=0.01, seed=5, device=0, bfs_mode=g.GS_BFS_MULTI)
+    eng.set_slots([1, 2])
+    eng.init_active_sets()
+    tdist.barrier()  # both processes hold an engine on the card
+    pers = bool(eng.info()["bfs_persistent"])
+    for r in range(6):
+        eng.round(r, record=True)
+    sm = eng.summaries()
+    eng.close()
+    np.savez(os.path.join(outdir, f"pb{rank}.npz"), pers=np.array([pers]), summ=sm.view(np.uint8))
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_processes_on_one_device_one_persistent_bfs():
+    """Two processes (gloo ranks) with one multi-BFS engine each on cuda:0: the persistent BFS
+    needs all its workgroups co-resident, so at most one process on a card may run it (a
+    lock named after the device's PCI bus id, gs_bfs_pers.hip); the other runs the launched
+    level loop. Exactly one of them reports the persistent path, and both runs' summaries are
+    equal (the two paths are bit-identical)."""
+    import torch.multiprocessing as mp
+    d = tempfile.mkdtemp()
+    mp.spawn(_pbfs_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+    outs = [np.load(os.path.join(d, f"pb{r}.npz")) for r in range(2)]
+    assert sum(bool(o["pers"][0]) for o in outs) == 1, [bool(o["pers"][0]) for o in outs]
+    assert outs[0]["summ"].tobytes() == outs[1]["summ"].tobytes()
+
+
 # ---- origin sharding of ONE network (bench.py --shard-origins, strong scaling) ----
 SH_N, SH_ORIGINS, SH_ROUNDS = 120, 7, 24
 
