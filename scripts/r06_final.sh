@@ -18,7 +18,10 @@ STEPS=${STEPS:-"pmc_c2 pmc_legs sq trace trace_default bench"}
 has() { case " $STEPS " in *" $1 "*) return 0;; *) return 1;; esac; }
 # (the box's profiles/r06 is read by the later steps' bench runs; only gpurun_out/ comes back:
 # every exit copies it there)
-trap 'mkdir -p $OUT/profiles_r06 && cp -r $P/. $OUT/profiles_r06/' EXIT
+# (only what this call wrote: a later call of a split run must not overwrite an earlier
+# call's fresh summaries with the tree's old ones)
+touch $OUT/.start_$$
+trap 'mkdir -p $OUT/profiles_r06 && find $P -maxdepth 1 -type f -newer $OUT/.start_$$ -exec cp {} $OUT/profiles_r06/ \;' EXIT
 
 if has pmc_c2; then
   for win in "5 20" "60 100" "20 100"; do  # (20 100: bench.py's defaults)
